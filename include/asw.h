@@ -1,0 +1,166 @@
+/*
+ * asw.h — C-ABI of the MI355X-native adaptive-support-weight (ASW) stereo matcher.
+ *
+ * Drop-in boundary for the reference's OpenCL `kernels/` path
+ * (manixq/stereo_matchin, stereo_matching/main.cpp:413-537).  Every entry point
+ * is `extern "C"`, takes plain pointers and sizes, returns an int status
+ * (ASW_OK or a negative ASW_E_* code; never throws), and names the reference
+ * interface it replaces.
+ *
+ * Two levels:
+ *   - STAGE API: device pointers, asynchronous on the caller's HIP stream
+ *     (`void* stream` is a hipStream_t; NULL = default stream).  One call per
+ *     reference kernel launch, with the same argument meaning.
+ *   - FRAME API: host RGBA8 pointers in, host disparity maps out, synchronous
+ *     (what main.cpp:183-186 -> :621-631 does for one image pair).
+ *
+ * Device data layout — NOT the reference's plane-major one:
+ *   images   : row-major RGBA8, [H][W][4]                         (as lodepng decodes)
+ *   cost     : PIXEL-major, [H][W][Dp] float32, Dp = asw_disp_pitch(p)
+ *              element (y,x,k) holds disparity d = p->d_begin + k (k < d_end-d_begin)
+ *   supports : [H][W][Tp] float32, Tp = asw_tap_pitch(p); element (y,x,i) = tap i
+ *   LUT      : [(R+1)][766] float32 support-weight table, R = (taps-1)/2
+ *   maps     : [H][W] int32 disparity indices, float32 confidences, u8 codes
+ */
+#ifndef ASW_H
+#define ASW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (main.cpp:27-30 ErCheck prints cl_int and continues; we return) ---- */
+#define ASW_OK 0
+#define ASW_E_INVALID -1     /* bad parameter / shape                         */
+#define ASW_E_HIP -2         /* a HIP runtime call failed (asw_last_hip_error) */
+#define ASW_E_NOMEM -3       /* device or host allocation failed              */
+#define ASW_E_UNSUPPORTED -4 /* parameter combination not built               */
+
+#define ASW_DIR_V 0 /* vertical pass / support   (asw_vSupport, asw_vCostAggregation) */
+#define ASW_DIR_H 1 /* horizontal pass / support (asw_hSupport, asw_hCostAggregation) */
+
+#define ASW_COLOR_RGB 0 /* reference: RGB sum of absolute differences (K/asw_vsupport.cl:22) */
+#define ASW_COLOR_LAB 1 /* extension (north star): CIELab Euclidean distance, unpinned       */
+
+#define ASW_LR_U8 0     /* parity: compare 8-bit codes like K/consist.cl:20-30 */
+#define ASW_LR_NATIVE 1 /* |d_ref - d_tar| <= 1 on integer indices (D > 256)   */
+
+/* Parameters.  asw_params_default() fills the reference values:
+ * ndisp 61 (K/asw_aggr.cl:16), taps 33 (K/asw_vcost_aggregation.cl:33), iters 7
+ * (main.cpp:177), gamma_c 30.91 / gamma_g 28.21 (K/asw_vsupport.cl:22,24),
+ * untruncated AD (tad_tau >= 765), LR check on with 8-bit codes. */
+typedef struct asw_params {
+    int width, height;   /* image size W, H                                    */
+    int ndisp;           /* D: disparity levels 0..D-1                          */
+    int taps;            /* T = 2R+1 taps per 1-D pass (odd)                    */
+    int iters;           /* r: (V,H) pass pairs                                 */
+    float gamma_c;       /* colour falloff                                       */
+    float gamma_g;       /* geometric falloff                                    */
+    int color_space;     /* ASW_COLOR_*                                          */
+    float tad_tau;       /* truncated-AD threshold; >= 765 is plain AD           */
+    int lr_check;        /* run the left-right consistency stage                */
+    int lr_mode;         /* ASW_LR_*                                             */
+    int d_begin, d_end;  /* disparity shard owned by this context [begin, end)  */
+} asw_params;
+
+void asw_params_default(asw_params *p);
+int asw_params_check(const asw_params *p);
+const char *asw_strerror(int status);
+int asw_last_hip_error(void); /* hipError_t of the last ASW_E_HIP */
+int asw_abi_version(void);
+
+/* layout helpers */
+int asw_disp_pitch(const asw_params *p); /* Dp = round_up(d_end-d_begin, 64)          */
+int asw_tap_pitch(const asw_params *p);  /* Tp = smallest 4k >= taps with k odd        */
+size_t asw_cost_bytes(const asw_params *p);    /* H*W*Dp*4   */
+size_t asw_support_bytes(const asw_params *p); /* H*W*Tp*4   */
+size_t asw_lut_bytes(const asw_params *p);     /* (R+1)*766*4 */
+
+/* ---------------- STAGE API (device pointers, async on `stream`) ---------------- */
+
+/* replaces asw_Aggr (K/asw_aggr.cl:3-23), launched at main.cpp:463-466:
+ * cost[y][x][k] = min(tad_tau, |dR|+|dG|+|dB|) between L(x,y) and R(max(x-d,0),y),
+ * d = d_begin + k; padding lanes k >= d_end-d_begin are written 0. */
+int asw_raw_cost(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba, float *cost,
+                 void *stream);
+
+/* support-weight table (the exp of K/asw_vsupport.cl:22-25 for every (|delta|, SAD)) */
+int asw_support_lut(const asw_params *p, float *lut, void *stream);
+
+/* replaces asw_vSupport / asw_hSupport (K/asw_vsupport.cl:3-27, K/asw_hsupport.cl:3-28),
+ * launched at main.cpp:469-484 (once per image and direction). */
+int asw_support(const asw_params *p, int dir, const uint8_t *img_rgba, const float *lut, float *w,
+                void *stream);
+
+/* replaces asw_vCostAggregation / asw_hCostAggregation (K/asw_vcost_aggregation.cl:11-44,
+ * K/asw_hcost_aggregation.cl:12-44), launched at main.cpp:494-509.  One pass over
+ * every local plane: cout = sum_i wl_i*wr_i(xr)*cin_i / sum_i wl_i*wr_i(xr).
+ * The reference's dead `denom` output is not produced.  cin != cout. */
+int asw_aggregate_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin,
+                       float *cout, void *stream);
+
+/* r x (V,H) ping-pong of main.cpp:486-515 on two caller buffers; the result
+ * ends in `c0` (c0 holds the raw cost on entry, c1 is scratch). */
+int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
+                  float *c0, float *c1, void *stream);
+
+/* replaces asw_WTA (K/asw_wta.cl:12-82), launched at main.cpp:517-526, for a context
+ * that owns the whole disparity range: left first-argmin + confidence, the
+ * bresenham target scan, and the 8-bit codes the reference writes to its images. */
+int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
+            float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, void *stream);
+
+/* replaces Constistency (K/consist.cl:3-34), launched at main.cpp:529-537.
+ * conf_ref / conf_tar are zeroed in place where inconsistent (RMW like the
+ * reference).  out_rgba / out_red_rgba are [H][W][4]; either may be NULL. */
+int asw_consistency(const asw_params *p, const int32_t *d_ref, const int32_t *d_tar, const uint8_t *code_ref,
+                    const uint8_t *code_tar, float *conf_ref, float *conf_tar, uint8_t *out_rgba,
+                    uint8_t *out_red_rgba, void *stream);
+
+/* ---- d-sharded WTA (no reference counterpart: the reference runs one device) ----
+ * key = (float_bits(m1) << 32) | index, reduced with an elementwise MIN across
+ * shards (RCCL ncclMin on int64; keys are positive).  Sequence per frame:
+ *   asw_wta_local      -> allreduce_min(key)   -> asw_wta_second(ref)  -> allreduce_min(m2)
+ *   asw_wta_target_local(key) -> allreduce_min(tkey) -> asw_wta_second(tar) -> allreduce_min(t2)
+ *   asw_wta_finalize.
+ * Exact: the result equals asw_wta on the unsharded volume bit for bit. */
+int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m1, float *m2, void *stream);
+int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *key_ref, int64_t *tkey,
+                         float *t1, float *t2, void *stream);
+int asw_wta_second(const asw_params *p, const int64_t *key_global, const int64_t *key_local, const float *m1,
+                   const float *m2, float *m2_contrib, void *stream);
+int asw_wta_finalize(const asw_params *p, const int64_t *key, const float *m2, const int64_t *tkey,
+                     const float *t2, int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar,
+                     uint8_t *code_ref, uint8_t *code_tar, void *stream);
+
+/* ---------------- FRAME API (host pointers, synchronous) ---------------- */
+
+typedef struct asw_ctx asw_ctx;
+
+typedef struct asw_outputs { /* caller-owned host arrays; any may be NULL */
+    int32_t *d_ref, *d_tar;  /* [H][W] disparity indices (left, right view)     */
+    float *conf_ref, *conf_tar;
+    uint8_t *disp_rgba;      /* [H][W][4] 8-bit disparity image (asw_left_wta)  */
+    uint8_t *lr_rgba;        /* [H][W][4] consistency output ("consistency_error") */
+    uint8_t *lr_red_rgba;    /* [H][W][4] asw_consistency_pre-reff.png image    */
+    float *cost;             /* [H][W][Dp] final aggregated volume (optional)   */
+} asw_outputs;
+
+typedef struct asw_timings { /* milliseconds from HIP events, columns of main.cpp:181 */
+    double raw_cost, support, v_pass_mean, h_pass_mean, aggregation_total, wta, consistency, total;
+    double h2d, d2h;
+} asw_timings;
+
+/* one context = one GPU (HIP device ordinal) and one disparity shard. */
+int asw_create(const asw_params *p, int hip_device, asw_ctx **out);
+int asw_destroy(asw_ctx *ctx);
+int asw_match(asw_ctx *ctx, const uint8_t *left_rgba, const uint8_t *right_rgba, asw_outputs *out,
+              asw_timings *t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASW_H */

@@ -1,0 +1,299 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C CPU restatement of the reference's adaptive-support-weight (ASW)
+ * hot path (manixq/stereo_matchin, OpenCL kernels under
+ * stereo_matching/kernels/, driven by stereo_matching/main.cpp:413-537).
+ * It exists to CHECK the HIP product path; it is never linked into, called
+ * by, or shipped with the product library.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.
+ *
+ * Pinning: the reference's own OpenCL sources cannot be built here without
+ * writing stand-ins for the OpenCL runtime builtins (read_imagef, get_global_id,
+ * ...), which this project does not do.  Instead this restatement is pinned
+ * against the reference's committed, device-produced outputs
+ * (stereo_matching/<scene>/asw_consistency_pre-reff.png for the five Middlebury
+ * scenes, captured as tests/golden/<scene>.npz by tests/golden/make_golden.py) —
+ * see tests/test_oracle_golden.py and DESIGN.md §Oracle.
+ *
+ * Layout: every volume is PLANE-MAJOR like the reference: [plane][y][x], x fastest.
+ * Images are row-major RGBA8 (what lodepng::decode hands main.cpp:183-186).
+ *
+ * Floating point: compiled with -ffp-contract=off; every fused multiply-add
+ * is an explicit fmaf() so the operation sequence is fixed (DESIGN.md §FP policy).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* fp policy for the aggregation tap update (DESIGN.md §FP policy):
+ *   0: num = num + ww*c ; den = den + ww           (no contraction)
+ *   1: num = fma(ww,c,num); den = den + ww          (contract the num update)
+ *   2: num = fma(ww,c,num); den = fma(wl,wr,den)    (aggressive contraction) */
+#define ORACLE_FMA_NONE 0
+#define ORACLE_FMA_NUM 1
+#define ORACLE_FMA_ALL 2
+
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+int oracle_version(void) { return 3; }
+
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
+}
+
+/* K/asw_aggr.cl:12-21 — C0[d][y][x] = (|dR|+|dG|)+|dB| between L(x,y) and
+ * R(clamp(x-d), y), read as float(c) (read_imagef(..)*255 == c exactly, and a
+ * sum of integers <= 765 is exact in fp32). */
+void oracle_raw_cost(const uint8_t *L, const uint8_t *R, int W, int H, int D, float *C) {
+    const long S = (long)W * H;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y) {
+        for (int d = 0; d < D; ++d) {
+            float *row = C + (long)d * S + (long)y * W;
+            for (int x = 0; x < W; ++x) {
+                const uint8_t *lp = L + 4 * ((long)y * W + x);
+                const uint8_t *rp = R + 4 * ((long)y * W + (x - d < 0 ? 0 : x - d));
+                float r = fabsf((float)lp[0] - (float)rp[0]) + fabsf((float)lp[1] - (float)rp[1]);
+                r = r + fabsf((float)lp[2] - (float)rp[2]);
+                row[x] = r;
+            }
+        }
+    }
+}
+
+/* K/asw_vsupport.cl:19-25 and K/asw_hsupport.cl:19-25:
+ *   c_diff = ((-1)*(|dr|+|dg|+|db|)) / gamma_c ; g_dist = distance(p,q) / gamma_g ;
+ *   w = exp(c_diff - g_dist)
+ * distance() of two integer points on one axis is |delta| exactly.
+ * exp is evaluated as (float)exp((double)arg) — correctly rounded in practice;
+ * the reference's vendor exp (<= 3 ulp by the OpenCL spec) is unpinned. */
+float oracle_support_weight(int sad, int dist, float gamma_c, float gamma_g) {
+    float c_diff = (float)(-sad) / gamma_c;
+    float g_dist = (float)dist / gamma_g;
+    float arg = c_diff - g_dist;
+    return (float)exp((double)arg);
+}
+
+/* dir 0 = vertical (asw_vSupport), 1 = horizontal (asw_hSupport).
+ * out is [T][H][W]; tap i pairs p=(x,y) with q = (x, clamp(y+i-R)) (V) or
+ * (clamp(x+i-R), y) (H). */
+void oracle_support(const uint8_t *img, int W, int H, int T, int dir, float gamma_c, float gamma_g,
+                    float *out) {
+    const int Rr = T / 2;
+    const long S = (long)W * H;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y) {
+        for (int i = 0; i < T; ++i) {
+            for (int x = 0; x < W; ++x) {
+                int qx = x, qy = y;
+                if (dir == 0) qy = clampi(y + i - Rr, 0, H - 1);
+                else qx = clampi(x + i - Rr, 0, W - 1);
+                const uint8_t *p = img + 4 * ((long)y * W + x);
+                const uint8_t *q = img + 4 * ((long)qy * W + qx);
+                int sad = abs((int)p[0] - q[0]) + abs((int)p[1] - q[1]) + abs((int)p[2] - q[2]);
+                int dist = dir == 0 ? abs(y - qy) : abs(x - qx);
+                out[(long)i * S + (long)y * W + x] = oracle_support_weight(sad, dist, gamma_c, gamma_g);
+            }
+        }
+    }
+}
+
+/* K/asw_vcost_aggregation.cl:23-42 (dir 0) and K/asw_hcost_aggregation.cl:24-43 (dir 1):
+ *   xr = max(x-d,0); num = den = 1e-5f;
+ *   for i in 0..T-1 (in order): ww = sL[i][y][x]*sR[i][y][xr];
+ *       num += ww * Cin[d][q]  (q = (x, clamp(y+i-R)) or (clamp(x+i-R), y)); den += ww;
+ *   Cout = num/den.
+ * The dead `denom` output of the reference is not produced.
+ * Voxels of planes [d0, d1) are computed; Cin/Cout are indexed by absolute plane
+ * relative to plane_base (Cin/Cout hold planes [plane_base, plane_base+nplanes)). */
+void oracle_pass(const float *sL, const float *sR, const float *Cin, float *Cout, int W, int H, int T,
+                 int dir, int d0, int d1, int plane_base, int fma_mode) {
+    const int Rr = T / 2;
+    const long S = (long)W * H;
+    const int nd = d1 - d0;
+#pragma omp parallel
+    {
+        float *num = (float *)malloc(sizeof(float) * W);
+        float *den = (float *)malloc(sizeof(float) * W);
+#pragma omp for schedule(static) collapse(2)
+        for (int dd = 0; dd < nd; ++dd) {
+            for (int y = 0; y < H; ++y) {
+                const int d = d0 + dd;
+                const float *cin = Cin + (long)(d - plane_base) * S;
+                float *cout = Cout + (long)(d - plane_base) * S + (long)y * W;
+                for (int x = 0; x < W; ++x) { num[x] = 1e-5f; den[x] = 1e-5f; }
+                for (int i = 0; i < T; ++i) {
+                    const float *wl = sL + (long)i * S + (long)y * W;
+                    const float *wr = sR + (long)i * S + (long)y * W;
+                    const float *crow;
+                    if (dir == 0) crow = cin + (long)clampi(y + i - Rr, 0, H - 1) * W;
+                    else crow = cin + (long)y * W;
+                    for (int x = 0; x < W; ++x) {
+                        const int xr = x - d < 0 ? 0 : x - d;
+                        const float a = wl[x];
+                        const float b = wr[xr];
+                        const float c = dir == 0 ? crow[x] : crow[clampi(x + i - Rr, 0, W - 1)];
+                        const float ww = a * b;
+                        if (fma_mode == ORACLE_FMA_NONE) {
+                            float t = ww * c;
+                            num[x] = num[x] + t;
+                            den[x] = den[x] + ww;
+                        } else if (fma_mode == ORACLE_FMA_NUM) {
+                            num[x] = fmaf(ww, c, num[x]);
+                            den[x] = den[x] + ww;
+                        } else {
+                            num[x] = fmaf(ww, c, num[x]);
+                            den[x] = fmaf(a, b, den[x]);
+                        }
+                    }
+                }
+                for (int x = 0; x < W; ++x) cout[x] = num[x] / den[x];
+            }
+        }
+        free(num);
+        free(den);
+    }
+}
+
+/* One sequential strict-'<' top-2 update (K/asw_wta.cl:43-46):
+ *   m2 = t<m2 ? t : m2 ; idx = t<m1 ? d : idx ; m2 = t<m1 ? m1 : m2 ; m1 = t<m1 ? t : m1
+ * m1 ends as the first minimum, m2 as the second smallest of the multiset. */
+#define TOP2_UPDATE(t, d, m1, m2, idx)           \
+    do {                                         \
+        float _t = (t);                          \
+        (m2) = _t < (m2) ? _t : (m2);            \
+        if (_t < (m1)) (idx) = (d);              \
+        (m2) = _t < (m1) ? (m1) : (m2);          \
+        (m1) = _t < (m1) ? _t : (m1);            \
+    } while (0)
+
+/* K/asw_wta.cl:22-80 (asw_WTA + bresenham, :3-9).
+ * Left ("reference") map: scan d = 0..D-1.  Right ("target") map: for i in
+ * 0..min_d-1, xq = max(0, x-i) and b = bresenham((0,x-min_d),(min_d,x),xq) which
+ * is always min_d + xq - x (slope (0-min_d)/((x-min_d)-x) == 1 in integer
+ * arithmetic); scan C[b][y][xq] with the same update; min_d_r starts at min_d.
+ * conf = (m2 - m1) / m2 (confidence_reference / confidence_target). */
+void oracle_wta(const float *C, int W, int H, int D, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
+                float *conf_tar) {
+    const long S = (long)W * H;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            const long p = (long)y * W + x;
+            float m1 = 100000.0f, m2 = 100000.0f;
+            int idx = 0;
+            for (int d = 0; d < D; ++d) TOP2_UPDATE(C[(long)d * S + p], d, m1, m2, idx);
+            const int md = idx;
+            float t1 = 100000.0f, t2 = 100000.0f;
+            int mdr = md;
+            for (int i = 0; i < md; ++i) {
+                const int xq = x - i < 0 ? 0 : x - i;
+                const int b = md + xq - x;
+                TOP2_UPDATE(C[(long)b * S + (long)y * W + xq], b, t1, t2, mdr);
+            }
+            d_ref[p] = md;
+            conf_ref[p] = (m2 - m1) / m2;
+            d_tar[p] = mdr;
+            conf_tar[p] = (t2 - t1) / t2;
+        }
+    }
+}
+
+/* UNORM8 code of a disparity index, K/asw_wta.cl:70-74: write_imagef of d/(D-1).
+ * Device convention (pinned by the committed PNGs): round half DOWN
+ * of 255*d/(D-1), computed exactly in integers: floor((510 d + D - 2) / (2 (D-1))).
+ * For D = 61 this is (17 d + 1) >> 2. */
+int oracle_code_u8(int d, int D) {
+    if (D <= 1) return 0;
+    long num = 510L * d + (D - 2);
+    long den = 2L * (D - 1);
+    long c = num / den;
+    return (int)(c > 255 ? 255 : (c < 0 ? 0 : c));
+}
+
+/* K/consist.cl:14-33 (Constistency): q = (code/255)*(D-1) per map, consistent iff
+ * |qR - qL| < 1.001f.  output_red = consistent ? ref : (255,0,0,255);
+ * output = consistent ? ref : tar; confidences zeroed where inconsistent (in place).
+ * (c/255)*(D-1)/(D-1) written back as UNORM8 returns c, so outputs are codes. */
+void oracle_consistency(const uint8_t *code_ref, const uint8_t *code_tar, float *conf_ref, float *conf_tar,
+                        int W, int H, int D, uint8_t *out_rgba, uint8_t *out_red_rgba) {
+    const long S = (long)W * H;
+    const float scale = (float)(D - 1);
+#pragma omp parallel for schedule(static)
+    for (long p = 0; p < S; ++p) {
+        const float qr = ((float)code_ref[p] / 255.0f) * scale;
+        const float qt = ((float)code_tar[p] / 255.0f) * scale;
+        const int cons = fabsf(qt - qr) < 1.001f;
+        uint8_t *o = out_rgba + 4 * p, *r = out_red_rgba + 4 * p;
+        const uint8_t cr = code_ref[p], ct = code_tar[p];
+        if (cons) {
+            o[0] = o[1] = o[2] = cr;
+            r[0] = r[1] = r[2] = cr;
+        } else {
+            o[0] = o[1] = o[2] = ct;
+            r[0] = 255; r[1] = 0; r[2] = 0;
+            conf_ref[p] = 0.0f;
+            conf_tar[p] = 0.0f;
+        }
+        o[3] = 255;
+        r[3] = 255;
+    }
+}
+
+/* main.cpp:463-537 — raw cost, 4 support launches, r x (V,H), WTA, consistency.
+ * Scratch is allocated here.  Outputs may be NULL when not wanted.
+ * cost_out (if not NULL) receives the final aggregated volume [D][H][W]. */
+int oracle_match(const uint8_t *L, const uint8_t *R, int W, int H, int D, int T, int iters, float gamma_c,
+                 float gamma_g, int fma_mode, int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar,
+                 uint8_t *out_rgba, uint8_t *out_red_rgba, float *cost_out) {
+    const long S = (long)W * H;
+    float *c0 = (float *)malloc(sizeof(float) * S * D);
+    float *c1 = (float *)malloc(sizeof(float) * S * D);
+    float *vl = (float *)malloc(sizeof(float) * S * T);
+    float *vr = (float *)malloc(sizeof(float) * S * T);
+    float *hl = (float *)malloc(sizeof(float) * S * T);
+    float *hr = (float *)malloc(sizeof(float) * S * T);
+    int32_t *dr = (int32_t *)malloc(sizeof(int32_t) * S);
+    int32_t *dt = (int32_t *)malloc(sizeof(int32_t) * S);
+    float *cr = (float *)malloc(sizeof(float) * S);
+    float *ct = (float *)malloc(sizeof(float) * S);
+    uint8_t *kr = (uint8_t *)malloc(S), *kt = (uint8_t *)malloc(S);
+    uint8_t *o1 = (uint8_t *)malloc(4 * S), *o2 = (uint8_t *)malloc(4 * S);
+    if (!c0 || !c1 || !vl || !vr || !hl || !hr || !dr || !dt || !cr || !ct || !kr || !kt || !o1 || !o2) return -1;
+    oracle_raw_cost(L, R, W, H, D, c0);
+    oracle_support(L, W, H, T, 0, gamma_c, gamma_g, vl);
+    oracle_support(L, W, H, T, 1, gamma_c, gamma_g, hl);
+    oracle_support(R, W, H, T, 0, gamma_c, gamma_g, vr);
+    oracle_support(R, W, H, T, 1, gamma_c, gamma_g, hr);
+    for (int it = 0; it < iters; ++it) {
+        oracle_pass(vl, vr, c0, c1, W, H, T, 0, 0, D, 0, fma_mode); /* V: c0 -> c1 */
+        oracle_pass(hl, hr, c1, c0, W, H, T, 1, 0, D, 0, fma_mode); /* H: c1 -> c0 */
+    }
+    oracle_wta(c0, W, H, D, dr, cr, dt, ct);
+    for (long p = 0; p < S; ++p) {
+        kr[p] = (uint8_t)oracle_code_u8(dr[p], D);
+        kt[p] = (uint8_t)oracle_code_u8(dt[p], D);
+    }
+    oracle_consistency(kr, kt, cr, ct, W, H, D, o1, o2);
+    if (d_ref) memcpy(d_ref, dr, sizeof(int32_t) * S);
+    if (d_tar) memcpy(d_tar, dt, sizeof(int32_t) * S);
+    if (conf_ref) memcpy(conf_ref, cr, sizeof(float) * S);
+    if (conf_tar) memcpy(conf_tar, ct, sizeof(float) * S);
+    if (out_rgba) memcpy(out_rgba, o1, 4 * S);
+    if (out_red_rgba) memcpy(out_red_rgba, o2, 4 * S);
+    if (cost_out) memcpy(cost_out, c0, sizeof(float) * S * D);
+    free(c0); free(c1); free(vl); free(vr); free(hl); free(hr);
+    free(dr); free(dt); free(cr); free(ct); free(kr); free(kt); free(o1); free(o2);
+    return 0;
+}

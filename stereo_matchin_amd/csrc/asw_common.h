@@ -1,0 +1,34 @@
+// Shared host/device definitions of the ASW matcher (layout pitches, error state).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "asw.h"
+
+namespace asw {
+
+constexpr int kWave = 64;
+constexpr int kSadMax = 765;        // 3 * 255: largest RGB SAD
+constexpr int kLutWidth = kSadMax + 1;
+
+// Tp: smallest multiple of 4 >= T whose quotient by 4 is odd.  A wave's lanes
+// read the support slab at a stride of Tp floats; an odd number of 16-byte
+// slots per row keeps ds_read_b128 conflict-free.
+__host__ __device__ constexpr int tap_pitch(int T) {
+    int k = (T + 3) / 4;
+    if ((k & 1) == 0) ++k;
+    return 4 * k;
+}
+
+__host__ __device__ constexpr int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+// 8-bit code of disparity index d for D levels: round-half-down of 255*d/(D-1),
+// the convention of the reference's write_imagef (K/asw_wta.cl:70-74).
+__host__ __device__ inline int code_u8(int d, int D) {
+    if (D <= 1) return 0;
+    long long c = (510LL * d + (D - 2)) / (2LL * (D - 1));
+    return c > 255 ? 255 : (c < 0 ? 0 : (int)c);
+}
+
+void set_hip_error(hipError_t e);
+
+}  // namespace asw

@@ -1,0 +1,752 @@
+// asw_kernels.hip — hand-written gfx950 (CDNA4) kernels of the ASW stereo hot path
+// and the STAGE half of the C-ABI declared in include/asw.h.
+//
+// Every kernel restates one reference OpenCL kernel (file:line in its comment)
+// with the same arithmetic, re-laid-out for MI355X:
+//   * cost volumes are PIXEL-major [H][W][Dp] (d fastest): a wave's 64 lanes are
+//     64 consecutive disparities of one pixel, so every cost load/store is one
+//     coalesced 256-byte access;
+//   * in an aggregation pass the left-image support weight of a tap is the same
+//     for the whole wave (one pixel) and comes from scalar loads (SGPR operand),
+//     while the right-image weight (column x-d differs per lane) is staged
+//     through LDS and read with ds_read_b128 (4 taps per read);
+//   * the 1-D cost window lives in VGPRs and rotates: each step loads ONE new
+//     cost element per lane and emits one output (no re-reads of the window).
+// FP policy (DESIGN.md §FP policy): per tap ww = wl*wr; num = fma(ww, c, num);
+// den = den + ww; taps in order i = 0..T-1; IEEE division num/den.
+// Compiled with -ffp-contract=off so the compiler adds no other contraction.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "asw_common.h"
+
+namespace asw {
+
+static thread_local int g_last_hip_error = 0;
+void set_hip_error(hipError_t e) { g_last_hip_error = (int)e; }
+
+namespace {
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// ---------------------------------------------------------------------------
+// Support-weight table.  w(sad, dist) = exp((-sad)/gamma_c - dist/gamma_g)
+// (K/asw_vsupport.cl:22-25): the weight depends only on the integer SAD and the
+// integer tap distance, so it is tabulated once per context.  exp is computed in
+// double with a fixed Cody-Waite + degree-14 Horner sequence and rounded to
+// float: correctly rounded on this domain (checked exhaustively against the
+// oracle by tests/test_gpu_parity.py::test_support_lut_exhaustive).
+// ---------------------------------------------------------------------------
+__device__ double exp_d(double x) {
+    const double inv_ln2 = 1.44269504088896338700e+00;
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double k = rint(x * inv_ln2);
+    double r = fma(-k, ln2_hi, x);
+    r = fma(-k, ln2_lo, r);
+    double p = 1.0 / 87178291200.0;  // 1/14!
+    p = fma(p, r, 1.0 / 6227020800.0);
+    p = fma(p, r, 1.0 / 479001600.0);
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)k);
+}
+
+__global__ void k_support_lut(float *lut, int rows, float gamma_c, float gamma_g) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= rows * kLutWidth) return;
+    const int dist = t / kLutWidth, sad = t % kLutWidth;
+    const float c_diff = (float)(-sad) / gamma_c;  // (-1)*(sum)/30.91f
+    const float g_dist = (float)dist / gamma_g;    // distance(p,q)/28.21f
+    const float arg = c_diff - g_dist;
+    lut[t] = (float)exp_d((double)arg);
+}
+
+// ---------------------------------------------------------------------------
+// asw_Aggr (K/asw_aggr.cl:3-23): per-disparity absolute-difference cost.
+// One thread per (pixel, local plane); d fastest => coalesced stores.
+// ---------------------------------------------------------------------------
+__global__ void k_raw_cost(const uchar4 *__restrict__ L, const uchar4 *__restrict__ R, float *__restrict__ cost,
+                           int W, int H, int Dp, int nloc, int d_begin, float tau) {
+    const long long n = (long long)W * H * Dp;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int k = (int)(idx % Dp);
+        const long long p = idx / Dp;
+        float v = 0.0f;
+        if (k < nloc) {
+            const int x = (int)(p % W), y = (int)(p / W);
+            const int d = d_begin + k;
+            const int xr = x - d < 0 ? 0 : x - d;
+            const uchar4 l = L[p];
+            const uchar4 r = R[(long long)y * W + xr];
+            float s = fabsf((float)l.x - (float)r.x) + fabsf((float)l.y - (float)r.y);
+            s = s + fabsf((float)l.z - (float)r.z);
+            v = fminf(s, tau);
+        }
+        cost[idx] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// asw_vSupport / asw_hSupport (K/asw_vsupport.cl:3-27, K/asw_hsupport.cl:3-28).
+// w[y][x][i] = LUT[|delta|][SAD(p,q)], q the i-th tap of p's 1-D window.
+// ---------------------------------------------------------------------------
+__global__ void k_support(const uchar4 *__restrict__ img, const float *__restrict__ lut, float *__restrict__ w,
+                          int W, int H, int T, int Tp, int dir) {
+    const long long n = (long long)W * H * Tp;
+    const int R = T / 2;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int i = (int)(idx % Tp);
+        const long long p = idx / Tp;
+        float v = 0.0f;
+        if (i < T) {
+            const int x = (int)(p % W), y = (int)(p / W);
+            int qx = x, qy = y, dist;
+            if (dir == ASW_DIR_V) {
+                qy = clampi(y + i - R, 0, H - 1);
+                dist = y > qy ? y - qy : qy - y;
+            } else {
+                qx = clampi(x + i - R, 0, W - 1);
+                dist = x > qx ? x - qx : qx - x;
+            }
+            const uchar4 a = img[p];
+            const uchar4 b = img[(long long)qy * W + qx];
+            const int sad = abs((int)a.x - (int)b.x) + abs((int)a.y - (int)b.y) + abs((int)a.z - (int)b.z);
+            v = lut[dist * kLutWidth + sad];
+        }
+        w[idx] = v;
+    }
+}
+
+// One tap of the weighted aggregation (K/asw_vcost_aggregation.cl:37-39).
+__device__ __forceinline__ void tap(float wl, float wr, float c, float &num, float &den) {
+    const float ww = wl * wr;
+    num = __builtin_fmaf(ww, c, num);
+    den = den + ww;
+}
+
+// ---------------------------------------------------------------------------
+// asw_vCostAggregation (K/asw_vcost_aggregation.cl:11-44).
+// Block = NW waves; wave w owns pixel column x = x0+w, lanes = 64 consecutive
+// local planes; the block walks a strip of rows.  Per row the block stages the
+// right-image support row for every xr = x-d it needs (NW+63 columns) into LDS
+// (double buffered, one barrier per row); the left support of (x,y) is
+// wave-uniform (scalar loads); the vertical cost window rotates in VGPRs.
+// ---------------------------------------------------------------------------
+template <int T, int NW>
+__global__ __launch_bounds__(NW * 64) void k_vpass(const float *__restrict__ wl, const float *__restrict__ wr,
+                                                   const float *__restrict__ cin, float *__restrict__ cout,
+                                                   int W, int H, int Dp, int d_begin, int rows_per_strip) {
+    constexpr int R = T / 2;
+    constexpr int TP = tap_pitch(T);
+    constexpr int Q = TP / 4;  // float4 per slab entry
+    constexpr int SLAB = NW + 63;
+    constexpr int NQ = SLAB * Q;
+    constexpr int NSTAGE = (NQ + NW * 64 - 1) / (NW * 64);
+    __shared__ float4 slab[2][NQ];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int x0 = blockIdx.x * NW;
+    const int kb = blockIdx.y * 64;
+    const int y_begin = blockIdx.z * rows_per_strip;
+    const int y_end = min(H, y_begin + rows_per_strip);
+    if (y_begin >= H) return;  // uniform for the whole block
+    const bool xvalid = x0 + wave < W;
+    const int x = min(x0 + wave, W - 1);
+    const int k = kb + lane;
+    const int dabs0 = d_begin + kb;
+    const int slab_base = x0 - dabs0 - 63;  // virtual xr of slab entry 0
+    const int e_lane = (x - x0) + 63 - lane;
+    const long long rowstride = (long long)W * Dp;
+    const float *cbase = cin + (long long)x * Dp + k;
+
+    float4 stage_v[NSTAGE];
+    auto stage_load = [&](int y) {
+#pragma unroll
+        for (int s = 0; s < NSTAGE; ++s) {
+            const int t = threadIdx.x + s * NW * 64;
+            if (t < NQ) {
+                const int e = t / Q, q = t - e * Q;
+                const int xr = clampi(slab_base + e, 0, W - 1);
+                stage_v[s] = *reinterpret_cast<const float4 *>(wr + ((long long)y * W + xr) * TP + 4 * q);
+            }
+        }
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int s = 0; s < NSTAGE; ++s) {
+            const int t = threadIdx.x + s * NW * 64;
+            if (t < NQ) slab[buf][t] = stage_v[s];
+        }
+    };
+
+    float win[T];
+#pragma unroll
+    for (int j = 0; j < T - 1; ++j) win[j] = cbase[clampi(y_begin - R + j, 0, H - 1) * rowstride];
+    stage_load(y_begin);
+    stage_store(0);
+    __syncthreads();
+
+    for (int ys = y_begin; ys < y_end; ys += T) {
+#pragma unroll
+        for (int s = 0; s < T; ++s) {
+            const int y = ys + s;
+            if (y >= y_end) break;
+            const int buf = (y - y_begin) & 1;
+            win[(s + T - 1) % T] = cbase[clampi(y + R, 0, H - 1) * rowstride];
+            const bool more = y + 1 < y_end;
+            if (more) stage_load(y + 1);
+            const float4 *srow = &slab[buf][e_lane * Q];
+            const float *wlrow = wl + ((long long)y * W + x) * TP;
+            float num = 1e-5f, den = 1e-5f;
+#pragma unroll
+            for (int i4 = 0; i4 < Q; ++i4) {
+                if (4 * i4 >= T) break;
+                const float4 r4 = srow[i4];
+                const float4 l4 = *reinterpret_cast<const float4 *>(wlrow + 4 * i4);
+                tap(l4.x, r4.x, win[(s + 4 * i4 + 0) % T], num, den);
+                if (4 * i4 + 1 < T) tap(l4.y, r4.y, win[(s + 4 * i4 + 1) % T], num, den);
+                if (4 * i4 + 2 < T) tap(l4.z, r4.z, win[(s + 4 * i4 + 2) % T], num, den);
+                if (4 * i4 + 3 < T) tap(l4.w, r4.w, win[(s + 4 * i4 + 3) % T], num, den);
+            }
+            if (xvalid) cout[(long long)y * rowstride + (long long)x * Dp + k] = num / den;
+            if (more) stage_store(buf ^ 1);
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// asw_hCostAggregation (K/asw_hcost_aggregation.cl:12-44).
+// Block = NW waves on one row y and a segment of NW*XW columns; lanes = 64
+// local planes.  The right-image support of every xr the segment needs
+// (NW*XW+63 columns) is staged into LDS once; each wave then sweeps XW columns
+// with the horizontal cost window rotating in VGPRs (no barriers in the sweep).
+// ---------------------------------------------------------------------------
+template <int T, int NW, int XW>
+__global__ __launch_bounds__(NW * 64) void k_hpass(const float *__restrict__ wl, const float *__restrict__ wr,
+                                                   const float *__restrict__ cin, float *__restrict__ cout,
+                                                   int W, int H, int Dp, int d_begin) {
+    constexpr int R = T / 2;
+    constexpr int TP = tap_pitch(T);
+    constexpr int Q = TP / 4;
+    constexpr int SEG = NW * XW;
+    constexpr int SLAB = SEG + 63;
+    constexpr int NQ = SLAB * Q;
+    __shared__ float4 slab[NQ];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int xs = blockIdx.x * SEG;
+    const int y = blockIdx.y;
+    const int kb = blockIdx.z * 64;
+    const int k = kb + lane;
+    const int dabs0 = d_begin + kb;
+    const int slab_base = xs - dabs0 - 63;
+
+    for (int t = threadIdx.x; t < NQ; t += NW * 64) {
+        const int e = t / Q, q = t - e * Q;
+        const int xr = clampi(slab_base + e, 0, W - 1);
+        slab[t] = *reinterpret_cast<const float4 *>(wr + ((long long)y * W + xr) * TP + 4 * q);
+    }
+    __syncthreads();
+
+    const int xw0 = xs + wave * XW;
+    if (xw0 >= W) return;
+    const int xw1 = min(xw0 + XW, W);
+    const float *cbase = cin + (long long)y * W * Dp + k;
+
+    float win[T];
+#pragma unroll
+    for (int j = 0; j < T - 1; ++j) win[j] = cbase[(long long)clampi(xw0 - R + j, 0, W - 1) * Dp];
+
+    for (int xb = xw0; xb < xw1; xb += T) {
+#pragma unroll
+        for (int s = 0; s < T; ++s) {
+            const int x = xb + s;
+            if (x >= xw1) break;
+            win[(s + T - 1) % T] = cbase[(long long)clampi(x + R, 0, W - 1) * Dp];
+            const float4 *srow = &slab[((x - xs) + 63 - lane) * Q];
+            const float *wlrow = wl + ((long long)y * W + x) * TP;
+            float num = 1e-5f, den = 1e-5f;
+#pragma unroll
+            for (int i4 = 0; i4 < Q; ++i4) {
+                if (4 * i4 >= T) break;
+                const float4 r4 = srow[i4];
+                const float4 l4 = *reinterpret_cast<const float4 *>(wlrow + 4 * i4);
+                tap(l4.x, r4.x, win[(s + 4 * i4 + 0) % T], num, den);
+                if (4 * i4 + 1 < T) tap(l4.y, r4.y, win[(s + 4 * i4 + 1) % T], num, den);
+                if (4 * i4 + 2 < T) tap(l4.z, r4.z, win[(s + 4 * i4 + 2) % T], num, den);
+                if (4 * i4 + 3 < T) tap(l4.w, r4.w, win[(s + 4 * i4 + 3) % T], num, den);
+            }
+            cout[((long long)y * W + x) * Dp + k] = num / den;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// WTA top-2 state: first minimum m1 (index idx) and the second smallest m2 of
+// the multiset, strict '<' in scan order (K/asw_wta.cl:43-46).  Partial states
+// over disjoint index sets combine exactly and order-independently:
+// m1 = lexicographic min of (value, index); m2 = min(max(m1a,m1b), m2a, m2b).
+// ---------------------------------------------------------------------------
+struct Top2 {
+    float m1, m2;
+    int idx;
+};
+
+__device__ __forceinline__ void top2_update(Top2 &s, float t, int d) {
+    s.m2 = t < s.m2 ? t : s.m2;
+    s.idx = t < s.m1 ? d : s.idx;
+    s.m2 = t < s.m1 ? s.m1 : s.m2;
+    s.m1 = t < s.m1 ? t : s.m1;
+}
+
+__device__ __forceinline__ void top2_combine(Top2 &a, float om1, float om2, int oidx) {
+    const float nm2 = fminf(fmaxf(a.m1, om1), fminf(a.m2, om2));
+    const bool take = (om1 < a.m1) || (om1 == a.m1 && oidx < a.idx);
+    a.m1 = take ? om1 : a.m1;
+    a.idx = take ? oidx : a.idx;
+    a.m2 = nm2;
+}
+
+__device__ __forceinline__ void top2_wave_reduce(Top2 &s) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float om1 = __shfl_xor(s.m1, off, 64);
+        const float om2 = __shfl_xor(s.m2, off, 64);
+        const int oidx = __shfl_xor(s.idx, off, 64);
+        top2_combine(s, om1, om2, oidx);
+    }
+}
+
+constexpr float kInit = 100000.0f;  // K/asw_wta.cl:25-26
+
+// Target (right-view) scan of asw_WTA (K/asw_wta.cl:50-67): for i < md,
+// xq = max(0,x-i), b = md + xq - x (the bresenham() line of :3-9 always has
+// slope 1), candidate C[b][y][xq].  Only b in [b_lo, b_hi) (the local shard) is
+// visited; `index` is i so ties keep the smallest i like the sequential scan.
+__device__ __forceinline__ Top2 target_scan(const float *__restrict__ cost, int x, int y, int W, int Dp, int md,
+                                            int b_lo, int b_hi, int lane) {
+    Top2 s{kInit, kInit, INT_MAX};
+    for (int i = lane; i < md; i += 64) {
+        const int xq = x - i < 0 ? 0 : x - i;
+        const int b = md + xq - x;
+        if (b >= b_lo && b < b_hi) {
+            const float t = cost[((long long)y * W + xq) * Dp + (b - b_lo)];
+            top2_update(s, t, i);
+        }
+    }
+    top2_wave_reduce(s);
+    return s;
+}
+
+// asw_WTA (K/asw_wta.cl:12-82) for a context owning all D planes.
+// One wave per pixel: lanes scan d = lane, lane+64, ... then a shuffle reduction.
+__global__ __launch_bounds__(256) void k_wta(const float *__restrict__ cost, int W, int H, int Dp, int D,
+                                             int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
+                                             int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
+                                             uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar) {
+    const int lane = threadIdx.x & 63;
+    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= (long long)W * H) return;
+    const int x = (int)(p % W), y = (int)(p / W);
+    const float *cp = cost + p * Dp;
+    Top2 s{kInit, kInit, INT_MAX};
+    for (int d = lane; d < D; d += 64) top2_update(s, cp[d], d);
+    top2_wave_reduce(s);
+    const int md = s.idx == INT_MAX ? 0 : s.idx;
+    const Top2 t = target_scan(cost, x, y, W, Dp, md, 0, D, lane);
+    if (lane == 0) {
+        const int mdr = t.idx == INT_MAX ? md : md + (x - t.idx < 0 ? 0 : x - t.idx) - x;
+        d_ref[p] = md;
+        conf_ref[p] = (s.m2 - s.m1) / s.m2;
+        d_tar[p] = mdr;
+        conf_tar[p] = (t.m2 - t.m1) / t.m2;
+        if (code_ref) code_ref[p] = (uint8_t)code_u8(md, D);
+        if (code_tar) code_tar[p] = (uint8_t)code_u8(mdr, D);
+    }
+}
+
+__device__ __forceinline__ long long make_key(float v, int idx) {
+    return (long long)(((unsigned long long)__float_as_uint(v) << 32) | (unsigned)idx);
+}
+constexpr long long kNoKey = 0x7fffffffffffffffLL;
+
+// d-sharded left WTA, local half: planes [d_begin, d_end) of the shard.
+__global__ __launch_bounds__(256) void k_wta_local(const float *__restrict__ cost, int W, int H, int Dp,
+                                                   int d_begin, int nloc, long long *__restrict__ key,
+                                                   float *__restrict__ m1, float *__restrict__ m2) {
+    const int lane = threadIdx.x & 63;
+    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= (long long)W * H) return;
+    const float *cp = cost + p * Dp;
+    Top2 s{kInit, kInit, INT_MAX};
+    for (int k = lane; k < nloc; k += 64) top2_update(s, cp[k], d_begin + k);
+    top2_wave_reduce(s);
+    if (lane == 0) {
+        key[p] = s.idx == INT_MAX ? kNoKey : make_key(s.m1, s.idx);
+        m1[p] = s.m1;
+        m2[p] = s.m2;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_wta_target_local(const float *__restrict__ cost, int W, int H, int Dp,
+                                                          int d_begin, int d_end,
+                                                          const long long *__restrict__ key_ref,
+                                                          long long *__restrict__ tkey, float *__restrict__ t1,
+                                                          float *__restrict__ t2) {
+    const int lane = threadIdx.x & 63;
+    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= (long long)W * H) return;
+    const int x = (int)(p % W), y = (int)(p / W);
+    const long long kr = key_ref[p];
+    const int md = kr == kNoKey ? 0 : (int)(unsigned)(kr & 0xffffffffLL);
+    const Top2 t = target_scan(cost, x, y, W, Dp, md, d_begin, d_end, lane);
+    if (lane == 0) {
+        tkey[p] = t.idx == INT_MAX ? kNoKey : make_key(t.m1, t.idx);
+        t1[p] = t.m1;
+        t2[p] = t.m2;
+    }
+}
+
+// second-smallest contribution: the shard that owns the global minimum offers
+// its own second smallest, every other shard its minimum.
+__global__ void k_wta_second(long long n, const long long *__restrict__ key_global,
+                             const long long *__restrict__ key_local, const float *__restrict__ m1,
+                             const float *__restrict__ m2, float *__restrict__ contrib) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    contrib[p] = key_local[p] == key_global[p] ? m2[p] : m1[p];
+}
+
+__global__ void k_wta_finalize(int W, int H, int D, const long long *__restrict__ key, const float *__restrict__ m2,
+                               const long long *__restrict__ tkey, const float *__restrict__ t2,
+                               int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
+                               int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
+                               uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (long long)W * H) return;
+    const int x = (int)(p % W);
+    const long long k = key[p], tk = tkey[p];
+    const int md = k == kNoKey ? 0 : (int)(unsigned)(k & 0xffffffffLL);
+    const float m1 = k == kNoKey ? kInit : __uint_as_float((unsigned)((unsigned long long)k >> 32));
+    int mdr = md;
+    float tm1 = kInit;
+    if (tk != kNoKey) {
+        const int i = (int)(unsigned)(tk & 0xffffffffLL);
+        mdr = md + (x - i < 0 ? 0 : x - i) - x;
+        tm1 = __uint_as_float((unsigned)((unsigned long long)tk >> 32));
+    }
+    d_ref[p] = md;
+    conf_ref[p] = (m2[p] - m1) / m2[p];
+    d_tar[p] = mdr;
+    conf_tar[p] = (t2[p] - tm1) / t2[p];
+    if (code_ref) code_ref[p] = (uint8_t)code_u8(md, D);
+    if (code_tar) code_tar[p] = (uint8_t)code_u8(mdr, D);
+}
+
+// Constistency (K/consist.cl:3-34).  The reference reads its 8-bit disparity
+// images back as q = (code/255)*60 and calls a pixel consistent iff
+// |q_tar - q_ref| < 1.001f; writing q/60 back to UNORM8 returns the code.
+__global__ void k_consistency(long long n, int D, int mode, const int32_t *__restrict__ d_ref,
+                              const int32_t *__restrict__ d_tar, const uint8_t *__restrict__ code_ref,
+                              const uint8_t *__restrict__ code_tar, float *__restrict__ conf_ref,
+                              float *__restrict__ conf_tar, uchar4 *__restrict__ out,
+                              uchar4 *__restrict__ out_red) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint8_t cr = code_ref[p], ct = code_tar[p];
+    bool cons;
+    if (mode == ASW_LR_U8) {
+        const float scale = (float)(D - 1);
+        const float qr = ((float)cr / 255.0f) * scale;
+        const float qt = ((float)ct / 255.0f) * scale;
+        cons = fabsf(qt - qr) < 1.001f;
+    } else {
+        const int dd = d_ref[p] - d_tar[p];
+        cons = dd <= 1 && dd >= -1;
+    }
+    if (!cons) {
+        conf_ref[p] = 0.0f;
+        conf_tar[p] = 0.0f;
+    }
+    if (out) out[p] = cons ? make_uchar4(cr, cr, cr, 255) : make_uchar4(ct, ct, ct, 255);
+    if (out_red) out_red[p] = cons ? make_uchar4(cr, cr, cr, 255) : make_uchar4(255, 0, 0, 255);
+}
+
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+inline int finish_launch() {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_hip_error(e);
+        return ASW_E_HIP;
+    }
+    return ASW_OK;
+}
+
+inline int grid_for(long long n, int block) {
+    long long g = (n + block - 1) / block;
+    return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
+
+template <int T>
+int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                  hipStream_t st) {
+    const int W = p->width, H = p->height;
+    const int Dp = asw_disp_pitch(p);
+    const int nkb = Dp / 64;
+    if (dir == ASW_DIR_V) {
+        constexpr int NW = 16;
+        const int nxb = (W + NW - 1) / NW;
+        // enough blocks to fill 256 CUs several times; strips >= 2T rows keep
+        // the window prologue (T-1 row loads per strip) a small overhead.
+        int nstrip = (int)((4096LL + (long long)nxb * nkb - 1) / ((long long)nxb * nkb));
+        const int max_strip = H / (2 * T) > 1 ? H / (2 * T) : 1;
+        if (nstrip > max_strip) nstrip = max_strip;
+        if (nstrip < 1) nstrip = 1;
+        const int rows = (H + nstrip - 1) / nstrip;
+        nstrip = (H + rows - 1) / rows;
+        hipLaunchKernelGGL((k_vpass<T, NW>), dim3(nxb, nkb, nstrip), dim3(NW * 64), 0, st, wl, wr, cin, cout, W, H,
+                           Dp, p->d_begin, rows);
+    } else {
+        constexpr int NW = 4;
+        constexpr int XW = (T > 41) ? 32 : 64;
+        constexpr int SEG = NW * XW;
+        const int nseg = (W + SEG - 1) / SEG;
+        hipLaunchKernelGGL((k_hpass<T, NW, XW>), dim3(nseg, H, nkb), dim3(NW * 64), 0, st, wl, wr, cin, cout, W, H,
+                           Dp, p->d_begin);
+    }
+    return finish_launch();
+}
+
+int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                hipStream_t st) {
+    switch (p->taps) {
+#define ASW_CASE(TT) \
+    case TT:         \
+        return launch_pass_t<TT>(p, dir, wl, wr, cin, cout, st);
+        ASW_CASE(3)
+        ASW_CASE(5)
+        ASW_CASE(7)
+        ASW_CASE(9)
+        ASW_CASE(15)
+        ASW_CASE(33)
+        ASW_CASE(35)
+        ASW_CASE(51)
+#undef ASW_CASE
+        default:
+            return ASW_E_UNSUPPORTED;
+    }
+}
+
+}  // namespace
+}  // namespace asw
+
+using namespace asw;
+
+// ===========================================================================
+// C-ABI: parameters and layout
+// ===========================================================================
+extern "C" {
+
+int asw_abi_version(void) { return 1; }
+
+void asw_params_default(asw_params *p) {
+    if (!p) return;
+    p->width = 0;
+    p->height = 0;
+    p->ndisp = 61;
+    p->taps = 33;
+    p->iters = 7;
+    p->gamma_c = 30.91f;
+    p->gamma_g = 28.21f;
+    p->color_space = ASW_COLOR_RGB;
+    p->tad_tau = 765.0f;
+    p->lr_check = 1;
+    p->lr_mode = ASW_LR_U8;
+    p->d_begin = 0;
+    p->d_end = -1;  // -1: = ndisp
+}
+
+static inline int d_end_of(const asw_params *p) { return p->d_end < 0 ? p->ndisp : p->d_end; }
+
+int asw_params_check(const asw_params *p) {
+    if (!p) return ASW_E_INVALID;
+    if (p->width < 1 || p->height < 1 || p->ndisp < 1 || p->taps < 1 || (p->taps & 1) == 0) return ASW_E_INVALID;
+    if (p->iters < 0 || !(p->gamma_c > 0.0f) || !(p->gamma_g > 0.0f)) return ASW_E_INVALID;
+    if (p->d_begin < 0 || d_end_of(p) > p->ndisp || p->d_begin >= d_end_of(p)) return ASW_E_INVALID;
+    if (p->color_space != ASW_COLOR_RGB) return ASW_E_UNSUPPORTED;
+    if (p->lr_mode != ASW_LR_U8 && p->lr_mode != ASW_LR_NATIVE) return ASW_E_INVALID;
+    if ((long long)p->width * p->height > (1LL << 31) / 64) return ASW_E_INVALID;
+    return ASW_OK;
+}
+
+const char *asw_strerror(int s) {
+    switch (s) {
+        case ASW_OK: return "ok";
+        case ASW_E_INVALID: return "invalid parameter";
+        case ASW_E_HIP: return "HIP runtime error";
+        case ASW_E_NOMEM: return "out of memory";
+        case ASW_E_UNSUPPORTED: return "unsupported parameter combination";
+        default: return "unknown status";
+    }
+}
+
+int asw_last_hip_error(void) { return g_last_hip_error; }
+
+int asw_disp_pitch(const asw_params *p) { return round_up(d_end_of(p) - p->d_begin, 64); }
+int asw_tap_pitch(const asw_params *p) { return tap_pitch(p->taps); }
+size_t asw_cost_bytes(const asw_params *p) {
+    return (size_t)p->width * p->height * (size_t)asw_disp_pitch(p) * sizeof(float);
+}
+size_t asw_support_bytes(const asw_params *p) {
+    return (size_t)p->width * p->height * (size_t)asw_tap_pitch(p) * sizeof(float);
+}
+size_t asw_lut_bytes(const asw_params *p) { return (size_t)(p->taps / 2 + 1) * kLutWidth * sizeof(float); }
+
+// ===========================================================================
+// C-ABI: stage API
+// ===========================================================================
+#define ASW_CHECK_PARAMS(p)                  \
+    do {                                     \
+        const int _s = asw_params_check(p);  \
+        if (_s != ASW_OK) return _s;         \
+    } while (0)
+
+int asw_raw_cost(const asw_params *p, const uint8_t *left, const uint8_t *right, float *cost, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!left || !right || !cost) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height * asw_disp_pitch(p);
+    hipLaunchKernelGGL(k_raw_cost, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uchar4 *>(left), reinterpret_cast<const uchar4 *>(right), cost,
+                       p->width, p->height, asw_disp_pitch(p), d_end_of(p) - p->d_begin, p->d_begin, p->tad_tau);
+    return finish_launch();
+}
+
+int asw_support_lut(const asw_params *p, float *lut, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!lut) return ASW_E_INVALID;
+    const int rows = p->taps / 2 + 1;
+    const int n = rows * kLutWidth;
+    hipLaunchKernelGGL(k_support_lut, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, lut, rows,
+                       p->gamma_c, p->gamma_g);
+    return finish_launch();
+}
+
+int asw_support(const asw_params *p, int dir, const uint8_t *img, const float *lut, float *w, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!img || !lut || !w || (dir != ASW_DIR_V && dir != ASW_DIR_H)) return ASW_E_INVALID;
+    const int Tp = asw_tap_pitch(p);
+    const long long n = (long long)p->width * p->height * Tp;
+    hipLaunchKernelGGL(k_support, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uchar4 *>(img), lut, w, p->width, p->height, p->taps, Tp, dir);
+    return finish_launch();
+}
+
+int asw_aggregate_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin,
+                       float *cout, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!wl || !wr || !cin || !cout || cin == cout || (dir != ASW_DIR_V && dir != ASW_DIR_H))
+        return ASW_E_INVALID;
+    return launch_pass(p, dir, wl, wr, cin, cout, (hipStream_t)stream);
+}
+
+int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
+                  float *c0, float *c1, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    for (int it = 0; it < p->iters; ++it) {
+        int s = asw_aggregate_pass(p, ASW_DIR_V, wvl, wvr, c0, c1, stream);
+        if (s != ASW_OK) return s;
+        s = asw_aggregate_pass(p, ASW_DIR_H, whl, whr, c1, c0, stream);
+        if (s != ASW_OK) return s;
+    }
+    return ASW_OK;
+}
+
+int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
+            float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (p->d_begin != 0 || d_end_of(p) != p->ndisp) return ASW_E_INVALID;  // sharded: use asw_wta_local & co.
+    if (!cost || !d_ref || !conf_ref || !d_tar || !conf_tar) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    hipLaunchKernelGGL(k_wta, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, cost, p->width,
+                       p->height, asw_disp_pitch(p), p->ndisp, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar);
+    return finish_launch();
+}
+
+int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m1, float *m2, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!cost || !key || !m1 || !m2) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    hipLaunchKernelGGL(k_wta_local, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, cost,
+                       p->width, p->height, asw_disp_pitch(p), p->d_begin, d_end_of(p) - p->d_begin,
+                       reinterpret_cast<long long *>(key), m1, m2);
+    return finish_launch();
+}
+
+int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *key_ref, int64_t *tkey, float *t1,
+                         float *t2, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!cost || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, cost,
+                       p->width, p->height, asw_disp_pitch(p), p->d_begin, d_end_of(p),
+                       reinterpret_cast<const long long *>(key_ref), reinterpret_cast<long long *>(tkey), t1, t2);
+    return finish_launch();
+}
+
+int asw_wta_second(const asw_params *p, const int64_t *key_global, const int64_t *key_local, const float *m1,
+                   const float *m2, float *m2_contrib, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!key_global || !key_local || !m1 || !m2 || !m2_contrib) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    hipLaunchKernelGGL(k_wta_second, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
+                       reinterpret_cast<const long long *>(key_global), reinterpret_cast<const long long *>(key_local),
+                       m1, m2, m2_contrib);
+    return finish_launch();
+}
+
+int asw_wta_finalize(const asw_params *p, const int64_t *key, const float *m2, const int64_t *tkey, const float *t2,
+                     int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar, uint8_t *code_ref,
+                     uint8_t *code_tar, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!key || !m2 || !tkey || !t2 || !d_ref || !conf_ref || !d_tar || !conf_tar) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    hipLaunchKernelGGL(k_wta_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       p->width, p->height, p->ndisp, reinterpret_cast<const long long *>(key), m2,
+                       reinterpret_cast<const long long *>(tkey), t2, d_ref, conf_ref, d_tar, conf_tar, code_ref,
+                       code_tar);
+    return finish_launch();
+}
+
+int asw_consistency(const asw_params *p, const int32_t *d_ref, const int32_t *d_tar, const uint8_t *code_ref,
+                    const uint8_t *code_tar, float *conf_ref, float *conf_tar, uint8_t *out_rgba,
+                    uint8_t *out_red_rgba, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!d_ref || !d_tar || !code_ref || !code_tar || !conf_ref || !conf_tar) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    hipLaunchKernelGGL(k_consistency, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
+                       p->ndisp, p->lr_mode, d_ref, d_tar, code_ref, code_tar, conf_ref, conf_tar,
+                       reinterpret_cast<uchar4 *>(out_rgba), reinterpret_cast<uchar4 *>(out_red_rgba));
+    return finish_launch();
+}
+
+}  // extern "C"

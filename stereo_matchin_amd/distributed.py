@@ -1,0 +1,122 @@
+"""Disparity-axis sharding of one stereo frame across GPUs (one process per GPU).
+
+The reference runs each OpenCL device independently (main.cpp:158-172); it has
+no multi-device path.  Here the frame's disparity range [0, D) is split into
+contiguous shards, one per rank (``torch.distributed``, backend "nccl" = RCCL
+over xGMI on MI355X):
+
+* raw cost, V and H passes of plane d read only plane d (plus the d-independent
+  supports), so every rank aggregates its own planes with NO communication;
+* the WTA over d is the one exchange step.  Each rank reduces its planes to a
+  partial top-2; partials combine exactly with elementwise MIN all-reduces of
+  ``key = (float_bits(m1) << 32) | index`` (ties -> smallest index, which is the
+  reference's first-argmin) and of the second-smallest contribution.  The
+  target-view scan (K/asw_wta.cl:50-67) needs the global left argmin, so it
+  follows the first exchange and repeats the pattern.  Four all-reduces per
+  frame: 2 x int64[H*W] + 2 x float32[H*W].
+
+The protocol (:func:`sharded_wta`) is written against two small interfaces so
+the same host logic runs on GPU tensors over RCCL (product) and on CPU tensors
+over gloo (tests/test_distributed.py).
+"""
+from __future__ import annotations
+
+from typing import Callable, Protocol
+
+import torch
+import torch.distributed as dist
+
+from . import kernels as K
+from ._lib import AswParams
+from .pipeline import MatchResult, StereoMatcher
+
+
+def shard_range(ndisp: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous balanced split of [0, ndisp) into `world` non-empty shards."""
+    if world > ndisp:
+        raise ValueError(f"cannot split {ndisp} disparities over {world} ranks")
+    base, rem = divmod(ndisp, world)
+    begin = rank * base + min(rank, rem)
+    return begin, begin + base + (1 if rank < rem else 0)
+
+
+class ShardOps(Protocol):
+    def local(self, cost): ...                    # -> key, m1, m2
+    def target_local(self, cost, key_ref): ...    # -> tkey, t1, t2
+    def second(self, key_g, key_l, m1, m2): ...   # -> contribution
+    def finalize(self, key, m2, tkey, t2): ...    # -> d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar
+
+
+def _allreduce_min_factory(group=None) -> Callable[[torch.Tensor], torch.Tensor]:
+    def reduce_min(t: torch.Tensor) -> torch.Tensor:
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        return t
+    return reduce_min
+
+
+def sharded_wta(ops: ShardOps, cost, reduce_min: Callable) -> tuple:
+    """Exact WTA over a d-sharded cost volume (see module doc)."""
+    key, m1, m2 = ops.local(cost)
+    key_g = reduce_min(key.clone())
+    m2_g = reduce_min(ops.second(key_g, key, m1, m2))
+    tkey, t1, t2 = ops.target_local(cost, key_g)
+    tkey_g = reduce_min(tkey.clone())
+    t2_g = reduce_min(ops.second(tkey_g, tkey, t1, t2))
+    return ops.finalize(key_g, m2_g, tkey_g, t2_g)
+
+
+class HipShardOps:
+    """The HIP C-ABI stage functions of include/asw.h for one shard."""
+
+    def __init__(self, p: AswParams):
+        self.p = p
+
+    def local(self, cost):
+        return K.wta_local(self.p, cost)
+
+    def target_local(self, cost, key_ref):
+        return K.wta_target_local(self.p, cost, key_ref)
+
+    def second(self, key_g, key_l, m1, m2):
+        return K.wta_second(self.p, key_g, key_l, m1, m2)
+
+    def finalize(self, key, m2, tkey, t2):
+        return K.wta_finalize(self.p, key, m2, tkey, t2)
+
+
+class ShardedStereoMatcher:
+    """One rank's share of a d-sharded frame."""
+
+    def __init__(self, params: AswParams, rank: int, world: int, device="cuda", group=None):
+        p = params.copy()
+        p.d_begin, p.d_end = shard_range(params.ndisp, rank, world)
+        self.p = p
+        self.rank, self.world = rank, world
+        self.matcher = StereoMatcher(p, device)
+        self.ops = HipShardOps(p)
+        self.reduce_min = _allreduce_min_factory(group)
+
+    def match(self, left: torch.Tensor, right: torch.Tensor, events: list | None = None) -> MatchResult:
+        m = self.matcher
+        if events is not None:
+            events.append(("start", _record()))
+        m.raw_and_support(left, right)
+        if events is not None:
+            events.append(("support", _record()))
+        cost = m.aggregate(events)
+        d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = sharded_wta(self.ops, cost, self.reduce_min)
+        if events is not None:
+            events.append(("wta", _record()))
+        lr = red = None
+        if self.p.lr_check:
+            lr, red = K.Constistency(self.p, d_ref, d_tar, code_ref, code_tar, conf_ref, conf_tar)
+        if events is not None:
+            events.append(("consistency", _record()))
+        return MatchResult(d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, lr, red, cost)
+
+
+def _record():
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e

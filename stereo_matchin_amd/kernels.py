@@ -1,0 +1,223 @@
+"""Reference-named operators on torch device tensors.
+
+One function per OpenCL kernel the reference enqueues on the ASW path
+(stereo_matching/main.cpp:463-537), with the same argument meaning, each a
+thin call into the HIP C-ABI (``include/asw.h``) on torch's current stream:
+
+=========================  ====================================  ==========================
+reference kernel           reference launch (main.cpp)           here
+=========================  ====================================  ==========================
+``asw_Aggr``               :463-466                               :func:`asw_Aggr`
+``asw_vSupport``           :469-472, :477-480                     :func:`asw_vSupport`
+``asw_hSupport``           :473-476, :481-484                     :func:`asw_hSupport`
+``asw_vCostAggregation``   :494-500 (x r)                         :func:`asw_vCostAggregation`
+``asw_hCostAggregation``   :503-509 (x r)                         :func:`asw_hCostAggregation`
+``asw_WTA``                :517-526                               :func:`asw_WTA`
+``Constistency``           :529-537                               :func:`Constistency`
+=========================  ====================================  ==========================
+
+Layouts are the MI355X ones of include/asw.h: images ``uint8 [H][W][4]``; cost
+volumes ``float32 [H][W][Dp]`` (pixel-major, disparity fastest); supports
+``float32 [H][W][Tp]``.  Errors raise :class:`~stereo_matchin_amd._lib.AswError`
+(the reference printed the cl_int and carried on, main.cpp:27-30).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import DIR_H, DIR_V, AswParams
+
+
+def _ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("ASW operators take device tensors (the HIP path has no CPU fallback)")
+    if not t.is_contiguous():
+        raise ValueError("ASW operators take contiguous tensors")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device | None = None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _expect(t: torch.Tensor, shape, dtype, name: str):
+    if tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype} {tuple(shape)}, got {t.dtype} {tuple(t.shape)}")
+
+
+def cost_shape(p: AswParams):
+    return (p.height, p.width, _lib.disp_pitch(p))
+
+
+def support_shape(p: AswParams):
+    return (p.height, p.width, _lib.tap_pitch(p))
+
+
+def lut_shape(p: AswParams):
+    return (p.taps // 2 + 1, 766)
+
+
+def new_cost(p: AswParams, device) -> torch.Tensor:
+    return torch.empty(cost_shape(p), dtype=torch.float32, device=device)
+
+
+def new_support(p: AswParams, device) -> torch.Tensor:
+    return torch.empty(support_shape(p), dtype=torch.float32, device=device)
+
+
+# --------------------------------------------------------------------------- stages
+
+def asw_Aggr(p: AswParams, left: torch.Tensor, right: torch.Tensor, out: torch.Tensor | None = None):
+    """Raw per-disparity cost (K/asw_aggr.cl:3-23) for planes [d_begin, d_end)."""
+    _expect(left, (p.height, p.width, 4), torch.uint8, "left")
+    _expect(right, (p.height, p.width, 4), torch.uint8, "right")
+    if out is None:
+        out = new_cost(p, left.device)
+    _expect(out, cost_shape(p), torch.float32, "out")
+    _lib.check(_lib.lib().asw_raw_cost(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(out), _stream(left.device)),
+               "asw_raw_cost")
+    return out
+
+
+def support_lut(p: AswParams, device, out: torch.Tensor | None = None) -> torch.Tensor:
+    """(R+1) x 766 table of exp(-sad/gamma_c - dist/gamma_g) (K/asw_vsupport.cl:22-25)."""
+    if out is None:
+        out = torch.empty(lut_shape(p), dtype=torch.float32, device=device)
+    _expect(out, lut_shape(p), torch.float32, "lut")
+    _lib.check(_lib.lib().asw_support_lut(ctypes.byref(p), _ptr(out), _stream(out.device)), "asw_support_lut")
+    return out
+
+
+def _support(p: AswParams, direction: int, img: torch.Tensor, lut: torch.Tensor | None, out):
+    _expect(img, (p.height, p.width, 4), torch.uint8, "image")
+    if lut is None:
+        lut = support_lut(p, img.device)
+    if out is None:
+        out = new_support(p, img.device)
+    _expect(out, support_shape(p), torch.float32, "out")
+    _lib.check(_lib.lib().asw_support(ctypes.byref(p), direction, _ptr(img), _ptr(lut), _ptr(out),
+                                      _stream(img.device)), "asw_support")
+    return out
+
+
+def asw_vSupport(p: AswParams, img: torch.Tensor, lut: torch.Tensor | None = None, out=None):
+    """Vertical support weights (K/asw_vsupport.cl:3-27)."""
+    return _support(p, DIR_V, img, lut, out)
+
+
+def asw_hSupport(p: AswParams, img: torch.Tensor, lut: torch.Tensor | None = None, out=None):
+    """Horizontal support weights (K/asw_hsupport.cl:3-28)."""
+    return _support(p, DIR_H, img, lut, out)
+
+
+def _pass(p: AswParams, direction: int, supp_left, supp_right, cost_in, out):
+    _expect(supp_left, support_shape(p), torch.float32, "supp_left")
+    _expect(supp_right, support_shape(p), torch.float32, "supp_right")
+    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
+    if out is None:
+        out = torch.empty_like(cost_in)
+    _expect(out, cost_shape(p), torch.float32, "out")
+    if out.data_ptr() == cost_in.data_ptr():
+        raise ValueError("aggregation passes are out of place (cost_in != out)")
+    _lib.check(_lib.lib().asw_aggregate_pass(ctypes.byref(p), direction, _ptr(supp_left), _ptr(supp_right),
+                                             _ptr(cost_in), _ptr(out), _stream(cost_in.device)),
+               "asw_aggregate_pass")
+    return out
+
+
+def asw_vCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None):
+    """One vertical weighted-aggregation pass (K/asw_vcost_aggregation.cl:11-44)."""
+    return _pass(p, DIR_V, supp_left, supp_right, cost_in, out)
+
+
+def asw_hCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None):
+    """One horizontal weighted-aggregation pass (K/asw_hcost_aggregation.cl:12-44)."""
+    return _pass(p, DIR_H, supp_left, supp_right, cost_in, out)
+
+
+def asw_WTA(p: AswParams, cost: torch.Tensor):
+    """Winner-take-all + target map (K/asw_wta.cl:12-82).
+
+    Returns ``(d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar)``: int32 index
+    maps, float32 confidences and the u8 codes the reference writes into its
+    ``asw_left_wta`` / ``asw_right_wta`` images.
+    """
+    _expect(cost, cost_shape(p), torch.float32, "cost")
+    H, W = p.height, p.width
+    dev = cost.device
+    d_ref = torch.empty((H, W), dtype=torch.int32, device=dev)
+    d_tar = torch.empty_like(d_ref)
+    conf_ref = torch.empty((H, W), dtype=torch.float32, device=dev)
+    conf_tar = torch.empty_like(conf_ref)
+    code_ref = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    code_tar = torch.empty_like(code_ref)
+    _lib.check(_lib.lib().asw_wta(ctypes.byref(p), _ptr(cost), _ptr(d_ref), _ptr(conf_ref), _ptr(d_tar),
+                                  _ptr(conf_tar), _ptr(code_ref), _ptr(code_tar), _stream(dev)), "asw_wta")
+    return d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar
+
+
+def Constistency(p: AswParams, d_ref, d_tar, code_ref, code_tar, conf_ref, conf_tar, want_rgba: bool = True):
+    """Left-right consistency (K/consist.cl:3-34).  Zeroes confidences in place.
+
+    Returns ``(output_rgba, output_red_rgba)`` — ``consistency_error`` and
+    ``consistency_error_red`` (the latter is asw_consistency_pre-reff.png).
+    """
+    H, W = p.height, p.width
+    dev = d_ref.device
+    out = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if want_rgba else None
+    red = torch.empty((H, W, 4), dtype=torch.uint8, device=dev) if want_rgba else None
+    _lib.check(_lib.lib().asw_consistency(ctypes.byref(p), _ptr(d_ref), _ptr(d_tar), _ptr(code_ref),
+                                          _ptr(code_tar), _ptr(conf_ref), _ptr(conf_tar), _ptr(out), _ptr(red),
+                                          _stream(dev)), "asw_consistency")
+    return out, red
+
+
+# ----------------------------------------------------------- sharded WTA primitives
+
+def wta_local(p: AswParams, cost):
+    H, W = p.height, p.width
+    dev = cost.device
+    key = torch.empty((H, W), dtype=torch.int64, device=dev)
+    m1 = torch.empty((H, W), dtype=torch.float32, device=dev)
+    m2 = torch.empty_like(m1)
+    _lib.check(_lib.lib().asw_wta_local(ctypes.byref(p), _ptr(cost), _ptr(key), _ptr(m1), _ptr(m2), _stream(dev)),
+               "asw_wta_local")
+    return key, m1, m2
+
+
+def wta_target_local(p: AswParams, cost, key_ref):
+    H, W = p.height, p.width
+    dev = cost.device
+    tkey = torch.empty((H, W), dtype=torch.int64, device=dev)
+    t1 = torch.empty((H, W), dtype=torch.float32, device=dev)
+    t2 = torch.empty_like(t1)
+    _lib.check(_lib.lib().asw_wta_target_local(ctypes.byref(p), _ptr(cost), _ptr(key_ref), _ptr(tkey), _ptr(t1),
+                                               _ptr(t2), _stream(dev)), "asw_wta_target_local")
+    return tkey, t1, t2
+
+
+def wta_second(p: AswParams, key_global, key_local, m1, m2):
+    out = torch.empty_like(m1)
+    _lib.check(_lib.lib().asw_wta_second(ctypes.byref(p), _ptr(key_global), _ptr(key_local), _ptr(m1), _ptr(m2),
+                                         _ptr(out), _stream(m1.device)), "asw_wta_second")
+    return out
+
+
+def wta_finalize(p: AswParams, key, m2, tkey, t2):
+    H, W = p.height, p.width
+    dev = key.device
+    d_ref = torch.empty((H, W), dtype=torch.int32, device=dev)
+    d_tar = torch.empty_like(d_ref)
+    conf_ref = torch.empty((H, W), dtype=torch.float32, device=dev)
+    conf_tar = torch.empty_like(conf_ref)
+    code_ref = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    code_tar = torch.empty_like(code_ref)
+    _lib.check(_lib.lib().asw_wta_finalize(ctypes.byref(p), _ptr(key), _ptr(m2), _ptr(tkey), _ptr(t2), _ptr(d_ref),
+                                           _ptr(conf_ref), _ptr(d_tar), _ptr(conf_tar), _ptr(code_ref),
+                                           _ptr(code_tar), _stream(dev)), "asw_wta_finalize")
+    return d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar

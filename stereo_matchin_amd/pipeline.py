@@ -1,0 +1,147 @@
+"""The ASW sequence of main.cpp:463-537 on one GPU, over the HIP C-ABI.
+
+:class:`StereoMatcher` owns the device buffers of one image size / parameter
+set (the reference re-creates every ``cl_mem`` per run, main.cpp:243-457; here
+they are allocated once and reused across frames) and runs
+
+    asw_Aggr -> 4 x support -> r x (V pass, H pass) -> asw_WTA -> Constistency
+
+on torch's current stream.  ``match()`` takes device-resident RGBA8 images.
+:func:`match_frame` is the host-pointer frame API (``asw_match``) used by the
+CLI path.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import kernels as K
+from ._lib import AswParams
+
+
+def make_params(width: int, height: int, ndisp: int = 61, taps: int = 33, iters: int = 7, **kw) -> AswParams:
+    """asw_params with the reference defaults (include/asw.h) and the given overrides."""
+    return _lib.default_params(width, height, ndisp=ndisp, taps=taps, iters=iters, **kw)
+
+
+@dataclass
+class MatchResult:
+    d_ref: torch.Tensor       # int32 [H][W] left-view disparity index
+    conf_ref: torch.Tensor    # float32 [H][W]
+    d_tar: torch.Tensor       # int32 [H][W] right-view (target) index
+    conf_tar: torch.Tensor
+    code_ref: torch.Tensor    # u8 [H][W] 8-bit image codes (asw_left_wta)
+    code_tar: torch.Tensor
+    lr_rgba: torch.Tensor | None       # consistency_error
+    lr_red_rgba: torch.Tensor | None   # consistency_error_red (asw_consistency_pre-reff.png)
+    cost: torch.Tensor        # final aggregated volume [H][W][Dp]
+
+
+class StereoMatcher:
+    def __init__(self, params: AswParams, device="cuda"):
+        st = _lib.params_check(params)
+        if st != _lib.ASW_OK:
+            raise _lib.AswError(st, "asw_params_check")
+        self.p = params.copy()
+        self.device = torch.device(device)
+        dev = self.device
+        self.lut = torch.empty(K.lut_shape(self.p), dtype=torch.float32, device=dev)
+        self.wvl = K.new_support(self.p, dev)
+        self.wvr = K.new_support(self.p, dev)
+        self.whl = K.new_support(self.p, dev)
+        self.whr = K.new_support(self.p, dev)
+        self.c0 = K.new_cost(self.p, dev)
+        self.c1 = K.new_cost(self.p, dev)
+
+    # -- stages ---------------------------------------------------------------
+    def raw_and_support(self, left: torch.Tensor, right: torch.Tensor):
+        p = self.p
+        K.asw_Aggr(p, left, right, out=self.c0)
+        K.support_lut(p, self.device, out=self.lut)
+        K.asw_vSupport(p, left, self.lut, out=self.wvl)
+        K.asw_hSupport(p, left, self.lut, out=self.whl)
+        K.asw_vSupport(p, right, self.lut, out=self.wvr)
+        K.asw_hSupport(p, right, self.lut, out=self.whr)
+
+    def aggregate(self, events: list | None = None):
+        """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515)."""
+        p = self.p
+        for _ in range(p.iters):
+            K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1)
+            if events is not None:
+                events.append(("v", _record()))
+            K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0)
+            if events is not None:
+                events.append(("h", _record()))
+        return self.c0
+
+    def match(self, left: torch.Tensor, right: torch.Tensor, lr_check: bool | None = None,
+              events: list | None = None) -> MatchResult:
+        p = self.p
+        if events is not None:
+            events.append(("start", _record()))
+        self.raw_and_support(left, right)
+        if events is not None:
+            events.append(("support", _record()))
+        cost = self.aggregate(events)
+        d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.asw_WTA(p, cost)
+        if events is not None:
+            events.append(("wta", _record()))
+        lr = red = None
+        if p.lr_check if lr_check is None else lr_check:
+            lr, red = K.Constistency(p, d_ref, d_tar, code_ref, code_tar, conf_ref, conf_tar)
+        if events is not None:
+            events.append(("consistency", _record()))
+        return MatchResult(d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, lr, red, cost)
+
+
+def _record():
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def to_rgba(img: np.ndarray) -> np.ndarray:
+    """RGB or RGBA u8 [H][W][C] -> contiguous RGBA8 (alpha 255), what lodepng::decode yields."""
+    img = np.asarray(img, np.uint8)
+    if img.ndim == 2:
+        img = np.repeat(img[..., None], 3, axis=2)
+    if img.shape[2] == 4:
+        return np.ascontiguousarray(img)
+    a = np.full(img.shape[:2] + (1,), 255, np.uint8)
+    return np.ascontiguousarray(np.concatenate([img[..., :3], a], axis=2))
+
+
+def match_frame(params: AswParams, left_rgba: np.ndarray, right_rgba: np.ndarray, device: int = 0,
+                want_cost: bool = False) -> dict:
+    """Frame API (``asw_create`` + ``asw_match``): host RGBA8 in, host maps out."""
+    L = _lib.lib()
+    H, W = params.height, params.width
+    left_rgba = to_rgba(left_rgba)
+    right_rgba = to_rgba(right_rgba)
+    assert left_rgba.shape == (H, W, 4) and right_rgba.shape == (H, W, 4)
+    ctx = ctypes.c_void_p()
+    _lib.check(L.asw_create(ctypes.byref(params), device, ctypes.byref(ctx)), "asw_create")
+    try:
+        out = {
+            "d_ref": np.empty((H, W), np.int32), "d_tar": np.empty((H, W), np.int32),
+            "conf_ref": np.empty((H, W), np.float32), "conf_tar": np.empty((H, W), np.float32),
+            "disp_rgba": np.empty((H, W, 4), np.uint8), "lr_rgba": np.empty((H, W, 4), np.uint8),
+            "lr_red_rgba": np.empty((H, W, 4), np.uint8),
+        }
+        if want_cost:
+            out["cost"] = np.empty((H, W, _lib.disp_pitch(params)), np.float32)
+        o = _lib.AswOutputs(*[out[k].ctypes.data if k in out else None for k in
+                              ("d_ref", "d_tar", "conf_ref", "conf_tar", "disp_rgba", "lr_rgba", "lr_red_rgba",
+                               "cost")])
+        t = _lib.AswTimings()
+        _lib.check(L.asw_match(ctx, left_rgba.ctypes.data, right_rgba.ctypes.data, ctypes.byref(o), ctypes.byref(t)),
+                   "asw_match")
+        out["timings"] = {f: getattr(t, f) for f, _ in t._fields_}
+        return out
+    finally:
+        L.asw_destroy(ctx)

@@ -1,0 +1,53 @@
+"""Generate the committed golden fixtures from the reference's own data files.
+
+Run in the survey/build container (where /root/reference exists):
+
+    python tests/golden/make_golden.py
+
+For each Middlebury scene listed in the reference's stereo_matching/pics.txt it
+stores, in ``tests/golden/<scene>.npz``:
+
+* ``left``, ``right``: the input pair as RGB u8 [H][W][3] (main.cpp:183-186 decodes
+  them with lodepng to RGBA8; alpha is 255 everywhere);
+* ``lr_red``: the reference's device-produced ``asw_consistency_pre-reff.png``
+  (RGB u8) — the output of ``Constistency`` right after the initial ASW WTA
+  (main.cpp:529-537, read back and encoded at :625-627).  This is the hot path's
+  own end-to-end output at the reference parameters D=61, T=33, r=7.
+
+These are data (inputs and expected outputs), not reference source.
+PNG decoding uses PIL, which is only needed to regenerate the fixtures.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+REF = "/root/reference/stereo_matching"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def main() -> int:
+    from PIL import Image
+
+    if not os.path.isdir(REF):
+        print("reference not present; nothing to do", file=sys.stderr)
+        return 1
+    with open(os.path.join(REF, "pics.txt")) as f:
+        lines = [ln.strip() for ln in f if ln.strip()]
+    pairs = list(zip(lines[0::2], lines[1::2]))
+    for lp, rp in pairs:
+        scene = lp.split("/")[0]
+        left = np.array(Image.open(os.path.join(REF, lp)).convert("RGB"))
+        right = np.array(Image.open(os.path.join(REF, rp)).convert("RGB"))
+        red = np.array(Image.open(os.path.join(REF, scene, "asw_consistency_pre-reff.png")).convert("RGB"))
+        assert left.shape == right.shape == red.shape, scene
+        np.savez_compressed(os.path.join(OUT, f"{scene}.npz"), left=left, right=right, lr_red=red,
+                            source=np.array(f"{lp} {rp} {scene}/asw_consistency_pre-reff.png"))
+        print(scene, left.shape)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,88 @@
+"""The C-ABI library loads and exports every symbol include/asw.h declares (CPU only:
+host-side helpers are called, no kernel is launched)."""
+import ctypes
+
+import pytest
+
+
+@pytest.fixture(scope="module")
+def L():
+    import stereo_matchin_amd._lib as L
+    L.lib()
+    return L
+
+
+def test_every_header_symbol_is_exported(L):
+    names = L.header_functions()
+    assert len(names) >= 20
+    lib = L.lib()
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes signature table covers exactly the header
+    assert set(names) == set(L.SIGNATURES)
+
+
+def test_abi_version(L):
+    assert L.lib().asw_abi_version() == 1
+
+
+def test_default_params_are_the_reference_values(L):
+    p = L.default_params(384, 288)
+    # K/asw_aggr.cl:16 (61 levels), K/asw_vcost_aggregation.cl:33 (33 taps), main.cpp:177 (r=7),
+    # K/asw_vsupport.cl:22,24 (30.91, 28.21), untruncated AD, LR check with 8-bit codes
+    assert (p.ndisp, p.taps, p.iters) == (61, 33, 7)
+    assert p.gamma_c == pytest.approx(30.91) and p.gamma_g == pytest.approx(28.21)
+    assert p.tad_tau >= 765.0 and p.lr_check == 1 and p.lr_mode == L.LR_U8
+    assert p.d_begin == 0 and p.d_stop == 61
+    assert L.params_check(p) == L.ASW_OK
+
+
+@pytest.mark.parametrize("D,T,Dp,Tp", [(61, 33, 64, 36), (16, 5, 64, 12), (64, 35, 64, 36), (256, 35, 256, 36),
+                                       (512, 51, 512, 52), (65, 3, 128, 4)])
+def test_layout_pitches(L, D, T, Dp, Tp):
+    p = L.default_params(100, 50, ndisp=D, taps=T)
+    assert L.disp_pitch(p) == Dp and L.tap_pitch(p) == Tp
+    assert (Tp // 4) % 2 == 1  # odd number of 16-B slots per support row (LDS banks)
+    lib = L.lib()
+    assert lib.asw_cost_bytes(ctypes.byref(p)) == 100 * 50 * Dp * 4
+    assert lib.asw_support_bytes(ctypes.byref(p)) == 100 * 50 * Tp * 4
+    assert lib.asw_lut_bytes(ctypes.byref(p)) == (T // 2 + 1) * 766 * 4
+
+
+def test_shard_pitch(L):
+    p = L.default_params(10, 10, ndisp=256, taps=35, d_begin=64, d_end=128)
+    assert L.disp_pitch(p) == 64
+    p = L.default_params(10, 10, ndisp=256, taps=35, d_begin=0, d_end=32)
+    assert L.disp_pitch(p) == 64
+
+
+@pytest.mark.parametrize("field,value", [("width", 0), ("height", -1), ("ndisp", 0), ("taps", 4), ("iters", -1),
+                                         ("gamma_c", 0.0), ("d_begin", 70), ("lr_mode", 7)])
+def test_params_check_rejects(L, field, value):
+    p = L.default_params(32, 32)
+    setattr(p, field, value)
+    assert L.params_check(p) == L.ASW_E_INVALID
+
+
+def test_unsupported_color_space(L):
+    p = L.default_params(32, 32, color_space=L.COLOR_LAB)
+    assert L.params_check(p) == L.ASW_E_UNSUPPORTED
+
+
+def test_strerror(L):
+    for s in (L.ASW_OK, L.ASW_E_INVALID, L.ASW_E_HIP, L.ASW_E_NOMEM, L.ASW_E_UNSUPPORTED):
+        assert L.strerror(s)
+    assert L.strerror(123) == "unknown status"
+
+
+def test_stage_api_validates_before_launch(L):
+    # invalid parameters / null pointers are rejected host-side, never launched
+    lib = L.lib()
+    p = L.default_params(0, 0)
+    assert lib.asw_raw_cost(ctypes.byref(p), None, None, None, None) == L.ASW_E_INVALID
+    p = L.default_params(8, 8)
+    assert lib.asw_raw_cost(ctypes.byref(p), None, None, None, None) == L.ASW_E_INVALID
+    assert lib.asw_aggregate_pass(ctypes.byref(p), 5, 1, 1, 1, 2, None) == L.ASW_E_INVALID
+    assert lib.asw_aggregate_pass(ctypes.byref(p), 0, 1, 1, 1, 1, None) == L.ASW_E_INVALID  # in place
+    p.d_end = 30
+    assert lib.asw_wta(ctypes.byref(p), 1, 1, 1, 1, 1, None, None, None) == L.ASW_E_INVALID  # sharded
