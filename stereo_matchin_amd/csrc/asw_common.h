@@ -31,4 +31,8 @@ __host__ __device__ inline int code_u8(int d, int D) {
 
 void set_hip_error(hipError_t e);
 
+// one aggregation pass over every local plane (asw_aggregate.hip)
+int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                hipStream_t st);
+
 }  // namespace asw

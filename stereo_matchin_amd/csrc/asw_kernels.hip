@@ -132,173 +132,6 @@ __global__ void k_support(const uchar4 *__restrict__ img, const float *__restric
     }
 }
 
-// One tap of the weighted aggregation (K/asw_vcost_aggregation.cl:37-39).
-__device__ __forceinline__ void tap(float wl, float wr, float c, float &num, float &den) {
-    const float ww = wl * wr;
-    num = __builtin_fmaf(ww, c, num);
-    den = den + ww;
-}
-
-// ---------------------------------------------------------------------------
-// asw_vCostAggregation (K/asw_vcost_aggregation.cl:11-44).
-// Block = NW waves; wave w owns pixel column x = x0+w, lanes = 64 consecutive
-// local planes; the block walks a strip of rows.  Per row the block stages the
-// right-image support row for every xr = x-d it needs (NW+63 columns) into LDS
-// (double buffered, one barrier per row); the left support of (x,y) is
-// wave-uniform (scalar loads); the vertical cost window rotates in VGPRs.
-// ---------------------------------------------------------------------------
-template <int T, int NW>
-__global__ __launch_bounds__(NW * 64) void k_vpass(const float *__restrict__ wl, const float *__restrict__ wr,
-                                                   const float *__restrict__ cin, float *__restrict__ cout,
-                                                   int W, int H, int Dp, int d_begin, int rows_per_strip) {
-    constexpr int R = T / 2;
-    constexpr int TP = tap_pitch(T);
-    constexpr int Q = TP / 4;  // float4 per slab entry
-    constexpr int SLAB = NW + 63;
-    constexpr int NQ = SLAB * Q;
-    constexpr int NSTAGE = (NQ + NW * 64 - 1) / (NW * 64);
-    __shared__ float4 slab[2][NQ];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int x0 = blockIdx.x * NW;
-    const int kb = blockIdx.y * 64;
-    const int y_begin = blockIdx.z * rows_per_strip;
-    const int y_end = min(H, y_begin + rows_per_strip);
-    if (y_begin >= H) return;  // uniform for the whole block
-    const bool xvalid = x0 + wave < W;
-    const int x = min(x0 + wave, W - 1);
-    const int k = kb + lane;
-    const int dabs0 = d_begin + kb;
-    const int slab_base = x0 - dabs0 - 63;  // virtual xr of slab entry 0
-    const int e_lane = (x - x0) + 63 - lane;
-    const long long rowstride = (long long)W * Dp;
-    const float *cbase = cin + (long long)x * Dp + k;
-
-    float4 stage_v[NSTAGE];
-    auto stage_load = [&](int y) {
-#pragma unroll
-        for (int s = 0; s < NSTAGE; ++s) {
-            const int t = threadIdx.x + s * NW * 64;
-            if (t < NQ) {
-                const int e = t / Q, q = t - e * Q;
-                const int xr = clampi(slab_base + e, 0, W - 1);
-                stage_v[s] = *reinterpret_cast<const float4 *>(wr + ((long long)y * W + xr) * TP + 4 * q);
-            }
-        }
-    };
-    auto stage_store = [&](int buf) {
-#pragma unroll
-        for (int s = 0; s < NSTAGE; ++s) {
-            const int t = threadIdx.x + s * NW * 64;
-            if (t < NQ) slab[buf][t] = stage_v[s];
-        }
-    };
-
-    float win[T];
-#pragma unroll
-    for (int j = 0; j < T - 1; ++j) win[j] = cbase[clampi(y_begin - R + j, 0, H - 1) * rowstride];
-    stage_load(y_begin);
-    stage_store(0);
-    __syncthreads();
-
-    for (int ys = y_begin; ys < y_end; ys += T) {
-#pragma unroll
-        for (int s = 0; s < T; ++s) {
-            const int y = ys + s;
-            if (y >= y_end) break;
-            const int buf = (y - y_begin) & 1;
-            win[(s + T - 1) % T] = cbase[clampi(y + R, 0, H - 1) * rowstride];
-            const bool more = y + 1 < y_end;
-            if (more) stage_load(y + 1);
-            const float4 *srow = &slab[buf][e_lane * Q];
-            const float *wlrow = wl + ((long long)y * W + x) * TP;
-            float num = 1e-5f, den = 1e-5f;
-#pragma unroll
-            for (int i4 = 0; i4 < Q; ++i4) {
-                if (4 * i4 >= T) break;
-                const float4 r4 = srow[i4];
-                const float4 l4 = *reinterpret_cast<const float4 *>(wlrow + 4 * i4);
-                tap(l4.x, r4.x, win[(s + 4 * i4 + 0) % T], num, den);
-                if (4 * i4 + 1 < T) tap(l4.y, r4.y, win[(s + 4 * i4 + 1) % T], num, den);
-                if (4 * i4 + 2 < T) tap(l4.z, r4.z, win[(s + 4 * i4 + 2) % T], num, den);
-                if (4 * i4 + 3 < T) tap(l4.w, r4.w, win[(s + 4 * i4 + 3) % T], num, den);
-            }
-            if (xvalid) cout[(long long)y * rowstride + (long long)x * Dp + k] = num / den;
-            if (more) stage_store(buf ^ 1);
-            __syncthreads();
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// asw_hCostAggregation (K/asw_hcost_aggregation.cl:12-44).
-// Block = NW waves on one row y and a segment of NW*XW columns; lanes = 64
-// local planes.  The right-image support of every xr the segment needs
-// (NW*XW+63 columns) is staged into LDS once; each wave then sweeps XW columns
-// with the horizontal cost window rotating in VGPRs (no barriers in the sweep).
-// ---------------------------------------------------------------------------
-template <int T, int NW, int XW>
-__global__ __launch_bounds__(NW * 64) void k_hpass(const float *__restrict__ wl, const float *__restrict__ wr,
-                                                   const float *__restrict__ cin, float *__restrict__ cout,
-                                                   int W, int H, int Dp, int d_begin) {
-    constexpr int R = T / 2;
-    constexpr int TP = tap_pitch(T);
-    constexpr int Q = TP / 4;
-    constexpr int SEG = NW * XW;
-    constexpr int SLAB = SEG + 63;
-    constexpr int NQ = SLAB * Q;
-    __shared__ float4 slab[NQ];
-
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int xs = blockIdx.x * SEG;
-    const int y = blockIdx.y;
-    const int kb = blockIdx.z * 64;
-    const int k = kb + lane;
-    const int dabs0 = d_begin + kb;
-    const int slab_base = xs - dabs0 - 63;
-
-    for (int t = threadIdx.x; t < NQ; t += NW * 64) {
-        const int e = t / Q, q = t - e * Q;
-        const int xr = clampi(slab_base + e, 0, W - 1);
-        slab[t] = *reinterpret_cast<const float4 *>(wr + ((long long)y * W + xr) * TP + 4 * q);
-    }
-    __syncthreads();
-
-    const int xw0 = xs + wave * XW;
-    if (xw0 >= W) return;
-    const int xw1 = min(xw0 + XW, W);
-    const float *cbase = cin + (long long)y * W * Dp + k;
-
-    float win[T];
-#pragma unroll
-    for (int j = 0; j < T - 1; ++j) win[j] = cbase[(long long)clampi(xw0 - R + j, 0, W - 1) * Dp];
-
-    for (int xb = xw0; xb < xw1; xb += T) {
-#pragma unroll
-        for (int s = 0; s < T; ++s) {
-            const int x = xb + s;
-            if (x >= xw1) break;
-            win[(s + T - 1) % T] = cbase[(long long)clampi(x + R, 0, W - 1) * Dp];
-            const float4 *srow = &slab[((x - xs) + 63 - lane) * Q];
-            const float *wlrow = wl + ((long long)y * W + x) * TP;
-            float num = 1e-5f, den = 1e-5f;
-#pragma unroll
-            for (int i4 = 0; i4 < Q; ++i4) {
-                if (4 * i4 >= T) break;
-                const float4 r4 = srow[i4];
-                const float4 l4 = *reinterpret_cast<const float4 *>(wlrow + 4 * i4);
-                tap(l4.x, r4.x, win[(s + 4 * i4 + 0) % T], num, den);
-                if (4 * i4 + 1 < T) tap(l4.y, r4.y, win[(s + 4 * i4 + 1) % T], num, den);
-                if (4 * i4 + 2 < T) tap(l4.z, r4.z, win[(s + 4 * i4 + 2) % T], num, den);
-                if (4 * i4 + 3 < T) tap(l4.w, r4.w, win[(s + 4 * i4 + 3) % T], num, den);
-            }
-            cout[((long long)y * W + x) * Dp + k] = num / den;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // WTA top-2 state: first minimum m1 (index idx) and the second smallest m2 of
 // the multiset, strict '<' in scan order (K/asw_wta.cl:43-46).  Partial states
@@ -507,56 +340,6 @@ inline int grid_for(long long n, int block) {
     return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
 }
 
-template <int T>
-int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                  hipStream_t st) {
-    const int W = p->width, H = p->height;
-    const int Dp = asw_disp_pitch(p);
-    const int nkb = Dp / 64;
-    if (dir == ASW_DIR_V) {
-        constexpr int NW = 16;
-        const int nxb = (W + NW - 1) / NW;
-        // enough blocks to fill 256 CUs several times; strips >= 2T rows keep
-        // the window prologue (T-1 row loads per strip) a small overhead.
-        int nstrip = (int)((4096LL + (long long)nxb * nkb - 1) / ((long long)nxb * nkb));
-        const int max_strip = H / (2 * T) > 1 ? H / (2 * T) : 1;
-        if (nstrip > max_strip) nstrip = max_strip;
-        if (nstrip < 1) nstrip = 1;
-        const int rows = (H + nstrip - 1) / nstrip;
-        nstrip = (H + rows - 1) / rows;
-        hipLaunchKernelGGL((k_vpass<T, NW>), dim3(nxb, nkb, nstrip), dim3(NW * 64), 0, st, wl, wr, cin, cout, W, H,
-                           Dp, p->d_begin, rows);
-    } else {
-        constexpr int NW = 4;
-        constexpr int XW = (T > 41) ? 32 : 64;
-        constexpr int SEG = NW * XW;
-        const int nseg = (W + SEG - 1) / SEG;
-        hipLaunchKernelGGL((k_hpass<T, NW, XW>), dim3(nseg, H, nkb), dim3(NW * 64), 0, st, wl, wr, cin, cout, W, H,
-                           Dp, p->d_begin);
-    }
-    return finish_launch();
-}
-
-int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                hipStream_t st) {
-    switch (p->taps) {
-#define ASW_CASE(TT) \
-    case TT:         \
-        return launch_pass_t<TT>(p, dir, wl, wr, cin, cout, st);
-        ASW_CASE(3)
-        ASW_CASE(5)
-        ASW_CASE(7)
-        ASW_CASE(9)
-        ASW_CASE(15)
-        ASW_CASE(33)
-        ASW_CASE(35)
-        ASW_CASE(51)
-#undef ASW_CASE
-        default:
-            return ASW_E_UNSUPPORTED;
-    }
-}
-
 }  // namespace
 }  // namespace asw
 
@@ -666,7 +449,7 @@ int asw_aggregate_pass(const asw_params *p, int dir, const float *wl, const floa
     ASW_CHECK_PARAMS(p);
     if (!wl || !wr || !cin || !cout || cin == cout || (dir != ASW_DIR_V && dir != ASW_DIR_H))
         return ASW_E_INVALID;
-    return launch_pass(p, dir, wl, wr, cin, cout, (hipStream_t)stream);
+    return asw::launch_pass(p, dir, wl, wr, cin, cout, (hipStream_t)stream);
 }
 
 int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
