@@ -136,6 +136,12 @@ int asw_wta_finalize(const asw_params *p, const int64_t *key, const float *m2, c
                      const float *t2, int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar,
                      uint8_t *code_ref, uint8_t *code_tar, void *stream);
 
+/* tuning hook (benchmarks / kernel experiments): selects among compiled kernel
+ * variants; returns the previous value, or ASW_E_INVALID for an unknown key.
+ * Every variant computes bit-identical results. */
+#define ASW_TUNE_PASS_VARIANT 1
+int asw_tune_set(int key, int value);
+
 /* ---------------- FRAME API (host pointers, synchronous) ---------------- */
 
 typedef struct asw_ctx asw_ctx;

@@ -34,5 +34,6 @@ void set_hip_error(hipError_t e);
 // one aggregation pass over every local plane (asw_aggregate.hip)
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                 hipStream_t st);
+int set_pass_variant(int v);
 
 }  // namespace asw

@@ -352,6 +352,11 @@ extern "C" {
 
 int asw_abi_version(void) { return 1; }
 
+int asw_tune_set(int key, int value) {
+    if (key == ASW_TUNE_PASS_VARIANT) return asw::set_pass_variant(value);
+    return ASW_E_INVALID;
+}
+
 void asw_params_default(asw_params *p) {
     if (!p) return;
     p->width = 0;
