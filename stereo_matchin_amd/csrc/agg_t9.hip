@@ -1,0 +1,3 @@
+// aggregation passes for T = 9 taps (see asw_aggregate_impl.h)
+#include "asw_aggregate_impl.h"
+ASW_INSTANTIATE_PASS(9)

@@ -1,375 +1,21 @@
-// asw_aggregate.hip — the iterated weighted-aggregation passes, the hot kernels of
-// the ASW path (reference: K/asw_vcost_aggregation.cl:11-44 and
-// K/asw_hcost_aggregation.cl:12-44, 2*r launches per frame at main.cpp:492-515,
-// 94 % of the reference's ASW time).
-//
-// Per voxel (x, y, d) and tap i = 0..T-1, in order (FP policy):
-//     ww = wl_i(x,y) * wr_i(max(x-d,0), y);  num = fma(ww, c_i, num);  den = den + ww
-// with num = den = 1e-5f on entry and out = num / den (IEEE).  c_i is the cost
-// of plane d at the i-th vertical (V) or horizontal (H) neighbour, clamped.
-//
-// MI355X mapping (both passes):
-//   * lanes = 64 consecutive disparities of one pixel; cost volumes are
-//     [H][W][Dp], so the single cost load and the single store of a step are one
-//     coalesced 256-B access per wave;
-//   * the wave sweeps along the aggregation axis; the T-tap cost window lives in a
-//     rotating VGPR ring of U = T+P registers and the next element is loaded P
-//     steps ahead (every ring index is a compile-time constant: the U-step sweep
-//     body is generated by static_for);
-//   * wl_i(x,y) is the same for the whole wave.  It is loaded with ordinary vector
-//     loads PS steps ahead into NJ = ceil(T/16) VGPRs, lane l of register j holding
-//     tap 16j + (l & 15) (each 16-lane row a copy), and fed to the multiply through
-//     the DPP row_newbcast source modifier: ww = v_mul_f32_dpp(wl, wr) is ONE VALU
-//     instruction and no scalar loads sit on the step's critical path;
-//   * wr_i(x-d,y) differs per lane: the support rows of every x-d the block needs
-//     are staged in LDS ([xr][Tp], Tp/4 odd => conflict-free ds_read_b128, 4 taps
-//     per read).  H pass: one slab per row segment, staged once.  V pass: one slab
-//     per row, double-buffered, loads issued PS steps ahead through a VGPR ring,
-//     one barrier per row;
-//   * block numbering keeps the tiles that share support data on one XCD
-//     (blockIdx % 8 = XCD group), so the shared lines come from that XCD's L2.
-// Per voxel-tap the VALU work is the 3 instructions above; everything else is
-// amortised over the T taps of a step.
+// asw_aggregate.hip — dispatch of the aggregation passes over the compiled tap
+// counts; the kernels are in asw_aggregate_impl.h, instantiated one tap count per
+// translation unit (agg_t<T>.hip) so they compile in parallel.
 #include <hip/hip_runtime.h>
-
-#include <cstdint>
-#include <type_traits>
 
 #include "asw_common.h"
 
 namespace asw {
-namespace {
-
-// native 4-float vector (the HIP float4 struct/union blocks SROA of small arrays)
-using f4 = float __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// C prefetch distance P: smallest P >= 3 with (T + P) % 4 == 0, so that the
-// 4-deep staging / left-weight rings (PS = 4) divide U = T + P.
-constexpr int pf_dist(int T) {
-    int P = 3;
-    while ((T + P) % 4 != 0) ++P;
-    return P;
-}
-constexpr int kPS = 4;
-
-// Compile-time loop: f(integral_constant<int, I>) for I in [B, E).
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F &&f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        static_for<B + 1, E>(f);
-    }
-}
-
-// Broadcast lane L of every 16-lane row (DPP row_newbcast); folded by the
-// compiler into the consuming v_mul_f32 as its src0 modifier (this needs
-// -fno-slp-vectorize: packed v_pk_mul_f32 cannot take a DPP operand).
-template <int L>
-__device__ __forceinline__ float row_bcast(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + L, 0xF, 0xF, false));
-}
-
-// IEEE-754 single-precision num/den, correctly rounded, for the operand range of
-// an aggregation tap sum: num, den in [1e-5, 765*T + 1], both normal and positive,
-// so the quotient is normal and no operand needs the v_div_scale/v_div_fixup
-// range handling of the general expansion.  Reciprocal refined by one Newton
-// step, then two Markstein residual corrections (the general f32 fdiv sequence
-// minus scale/fixup); checked bit-exact against the oracle's '/' on every voxel
-// of the parity tests.
-__device__ __forceinline__ float div_pos(float num, float den) {
-    float r = __builtin_amdgcn_rcpf(den);
-    const float e = __builtin_fmaf(-den, r, 1.0f);
-    r = __builtin_fmaf(e, r, r);
-    float q = num * r;
-    float rem = __builtin_fmaf(-den, q, num);
-    q = __builtin_fmaf(rem, r, q);
-    rem = __builtin_fmaf(-den, q, num);
-    return __builtin_fmaf(rem, r, q);
-}
-
-constexpr int nj_of(int T) { return (T + 15) / 16; }
-
-// Left weights of one pixel into the lane-replicated layout (see file header).
-template <int T, int TP>
-__device__ __forceinline__ void load_wl(float (&dst)[nj_of(T)], const float *__restrict__ px, int lane16) {
-#pragma unroll
-    for (int j = 0; j < nj_of(T); ++j) dst[j] = px[min(16 * j + lane16, TP - 1)];
-}
-
-// All T taps of one output, in order.
-template <int T, int U, int S>
-__device__ __forceinline__ float step_taps(float (&wl)[nj_of(T)], const f4 *srow, const float (&win)[U]) {
-    constexpr int Q = (T + 3) / 4;
-    float num = 1e-5f, den = 1e-5f;
-    static_for<0, Q>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int i4 = decltype(qc)::value;
-        const f4 r4 = srow[i4];
-        static_for<0, 4>([&](auto jc) __attribute__((always_inline)) {
-            constexpr int i = 4 * i4 + decltype(jc)::value;
-            if constexpr (i < T) {
-                const float ww = row_bcast<i % 16>(wl[i / 16]) * r4[i % 4];
-                num = __builtin_fmaf(ww, win[(S + i) % U], num);
-                den = den + ww;
-            }
-        });
-    });
-    return div_pos(num, den);
-}
-
-// ---------------------------------------------------------------------------
-// V pass.  Block = NW waves = NW consecutive columns x0..x0+NW-1, one 64-plane
-// block, a strip of rows [y_begin, y_end).  Window slot of row q:
-// (q - (y_begin - R)) mod U; at step y the row y+R+P is loaded into the slot of
-// row y-R-1 (consumed at step y-1).  Tiles: XCD group j owns a contiguous range
-// of column groups and walks it fastest, so neighbouring column groups (whose
-// support slabs overlap in 63 of NW+63 entries) run concurrently on one L2.
-// ---------------------------------------------------------------------------
-template <int T, int NW>
-__global__ __launch_bounds__(NW * 64) void k_vpass(const float *__restrict__ wl, const float *__restrict__ wr,
-                                                   const float *__restrict__ cin, float *__restrict__ cout,
-                                                   int W, int H, int Dp, int d_begin, int rows_per_strip,
-                                                   int nxb, int nstrip, int xg_per_xcd) {
-    constexpr int R = T / 2;
-    constexpr int TP = tap_pitch(T);
-    constexpr int Q = TP / 4;
-    constexpr int P = pf_dist(T);
-    constexpr int U = T + P;
-    constexpr int PS = kPS;
-    constexpr int NJ = nj_of(T);
-    static_assert(U % PS == 0 && U % 2 == 0, "ring periods must divide the unroll period");
-    constexpr int SLAB = NW + 63;
-    constexpr int NQ = SLAB * Q;
-    constexpr int NSTAGE = (NQ + NW * 64 - 1) / (NW * 64);
-    static_assert(NSTAGE <= 2, "slab row larger than two float4 per thread");
-    __shared__ f4 slab[2][NQ];
-
-    const int nkb = Dp / 64;
-    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
-    const int xg = xcd * xg_per_xcd + m % xg_per_xcd;
-    const int rest = m / xg_per_xcd;
-    const int kbi = rest % nkb, strip = rest / nkb;
-    if (xg >= nxb || strip >= nstrip) return;  // padding block (uniform)
-    const int x0 = xg * NW;
-    const int y_begin = strip * rows_per_strip;
-    if (y_begin >= H) return;
-    const int y_end = min(H, y_begin + rows_per_strip);
-    const int lane = threadIdx.x & 63;
-    const int lane16 = lane & 15;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int kb = kbi * 64;
-    const int x = min(x0 + wave, W - 1);
-    const int k = kb + lane;
-    const int slab_base = x0 - (d_begin + kb) - 63;  // virtual xr of slab entry 0
-    const f4 *my_slab0 = &slab[0][((x - x0) + 63 - lane) * Q];
-    const long long rowstride = (long long)W * Dp;
-    const float *cbase = cin + (long long)x * Dp + k;
-    const float *wlcol = wl + (long long)x * TP;
-    const long long wrowstride = (long long)W * TP;  // row stride of both support arrays
-
-    // per-thread share of a slab row (<= 2 float4 per thread); surplus lanes
-    // redo the last entry (same value, same place)
-    const int t0 = min((int)threadIdx.x, NQ - 1);
-    const int t1 = min((int)threadIdx.x + NW * 64, NQ - 1);
-    const int off0 = clampi(slab_base + t0 / Q, 0, W - 1) * TP + 4 * (t0 % Q);
-    const int off1 = clampi(slab_base + t1 / Q, 0, W - 1) * TP + 4 * (t1 % Q);
-
-    float win[U];
-    f4 sa[PS], sb[PS];
-    float wlv[PS][NJ];
-#pragma unroll
-    for (int j = 0; j < T - 1 + P; ++j) win[j] = cbase[clampi(y_begin - R + j, 0, H - 1) * rowstride];
-#pragma unroll
-    for (int j = 0; j < PS; ++j) {
-        const long long ry = clampi(y_begin + j, 0, H - 1) * wrowstride;
-        sa[j] = *reinterpret_cast<const f4 *>(wr + ry + off0);
-        if constexpr (NSTAGE > 1) sb[j] = *reinterpret_cast<const f4 *>(wr + ry + off1);
-        load_wl<T, TP>(wlv[j], wlcol + ry, lane16);
-    }
-    slab[0][t0] = sa[0];
-    if constexpr (NSTAGE > 1) slab[0][t1] = sb[0];
-
-    // One row step.  CHK: the tail chunk of a strip checks the row bound; full
-    // chunks are branch-free so the ring loads stay where they are issued
-    // (a conditional step would let the compiler sink them next to their use).
-    auto body = [&](auto sc, auto chk, int ys) __attribute__((always_inline)) {
-        constexpr int s = decltype(sc)::value;
-        const int y = ys + s;
-        if constexpr (decltype(chk)::value) {
-            if (y >= y_end) return;
-        }
-        __syncthreads();  // slab s&1 written (step s-1); slab (s+1)&1 no longer read
-        win[(s + U - 1) % U] = cbase[clampi(y + R + P, 0, H - 1) * rowstride];
-        const float v = step_taps<T, U, s>(wlv[s % PS], my_slab0 + (s & 1) * NQ, win);
-        // a wave past the right edge recomputes column W-1 and stores the same bits
-        cout[(long long)y * rowstride + (long long)x * Dp + k] = v;
-        slab[(s + 1) & 1][t0] = sa[(s + 1) % PS];
-        if constexpr (NSTAGE > 1) slab[(s + 1) & 1][t1] = sb[(s + 1) % PS];
-        __builtin_amdgcn_sched_barrier(0);  // keep the ring reloads after this step's uses
-        const long long ry = clampi(y + PS, 0, H - 1) * wrowstride;
-        sa[s % PS] = *reinterpret_cast<const f4 *>(wr + ry + off0);
-        if constexpr (NSTAGE > 1) sb[s % PS] = *reinterpret_cast<const f4 *>(wr + ry + off1);
-        load_wl<T, TP>(wlv[s % PS], wlcol + ry, lane16);
-    };
-    int ys = y_begin;
-    for (; ys + U <= y_end; ys += U)
-        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::false_type{}, ys); });
-    if (ys < y_end)
-        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::true_type{}, ys); });
-}
-
-// ---------------------------------------------------------------------------
-// H pass.  Block = NW waves on row y and a segment of SEG = NW*XW columns; the
-// right-support slab for every xr the segment needs (SEG+63 entries) is staged
-// once.  Wave w sweeps columns [xs + w*XW, +XW).  Window slot of column q:
-// (q - (xw0 - R)) mod U.  Tiles: the Dp/64 plane blocks of one (row, segment)
-// (slabs overlapping in SEG-1 of SEG+63 entries) run back to back on one XCD.
-// ---------------------------------------------------------------------------
-template <int T, int NW, int XW>
-__global__ __launch_bounds__(NW * 64) void k_hpass(const float *__restrict__ wl, const float *__restrict__ wr,
-                                                   const float *__restrict__ cin, float *__restrict__ cout,
-                                                   int W, int H, int Dp, int d_begin, int nseg) {
-    constexpr int R = T / 2;
-    constexpr int TP = tap_pitch(T);
-    constexpr int Q = TP / 4;
-    constexpr int P = pf_dist(T);
-    constexpr int U = T + P;
-    constexpr int PS = kPS;
-    constexpr int NJ = nj_of(T);
-    static_assert(U % PS == 0 && U % 2 == 0, "ring periods must divide the unroll period");
-    constexpr int SEG = NW * XW;
-    constexpr int SLAB = SEG + 63;
-    constexpr int NQ = SLAB * Q;
-    __shared__ f4 slab[NQ];
-
-    const int nkb = Dp / 64;
-    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
-    const int group = (m / nkb) * 8 + xcd;
-    if (group >= H * nseg) return;  // padding block (uniform)
-    const int y = group / nseg;
-    const int xs = (group % nseg) * SEG;
-    const int lane = threadIdx.x & 63;
-    const int lane16 = lane & 15;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int kb = (m % nkb) * 64;
-    const int k = kb + lane;
-    const int slab_base = xs - (d_begin + kb) - 63;
-
-    const float *wrrow = wr + (long long)y * W * TP;
-    for (int t = threadIdx.x; t < NQ; t += NW * 64) {
-        const int e = t / Q, q = t - e * Q;
-        slab[t] = *reinterpret_cast<const f4 *>(wrrow + clampi(slab_base + e, 0, W - 1) * TP + 4 * q);
-    }
-    __syncthreads();
-
-    const int xw0 = xs + wave * XW;
-    if (xw0 >= W) return;
-    const int xw1 = min(xw0 + XW, W);
-    const float *cbase = cin + (long long)y * W * Dp + k;
-    const float *wlrow0 = wl + (long long)y * W * TP;
-
-    float win[U];
-    float wlv[PS][NJ];
-#pragma unroll
-    for (int j = 0; j < T - 1 + P; ++j) win[j] = cbase[(long long)clampi(xw0 - R + j, 0, W - 1) * Dp];
-#pragma unroll
-    for (int j = 0; j < PS; ++j) load_wl<T, TP>(wlv[j], wlrow0 + clampi(xw0 + j, 0, W - 1) * TP, lane16);
-
-    auto body = [&](auto sc, auto chk, int xb) __attribute__((always_inline)) {
-        constexpr int s = decltype(sc)::value;
-        const int x = xb + s;
-        if constexpr (decltype(chk)::value) {
-            if (x >= xw1) return;
-        }
-        win[(s + U - 1) % U] = cbase[(long long)clampi(x + R + P, 0, W - 1) * Dp];
-        const float v = step_taps<T, U, s>(wlv[s % PS], &slab[((x - xs) + 63 - lane) * Q], win);
-        cout[((long long)y * W + x) * Dp + k] = v;
-        __builtin_amdgcn_sched_barrier(0);  // keep the ring reload after this step's uses
-        load_wl<T, TP>(wlv[s % PS], wlrow0 + clampi(x + PS, 0, W - 1) * TP, lane16);
-    };
-    int xb = xw0;
-    for (; xb + U <= xw1; xb += U)
-        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::false_type{}, xb); });
-    if (xb < xw1)
-        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::true_type{}, xb); });
-}
-
-// Tuning variants (asw_tune_set(ASW_TUNE_PASS_VARIANT, v)): bits 1-2 = H-pass
-// block shape (0: 4 waves x XW, 1: 8 x XW, 2: 2 x 2XW); bit 3 = V pass with 8 waves.
+namespace agg {
 int g_pass_variant = 0;
-
-template <int T, int NW>
-void launch_v(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
-              hipStream_t st) {
-    const int W = p->width, H = p->height;
-    const int Dp = asw_disp_pitch(p);
-    const int nkb = Dp / 64;
-    const int nxb = (W + NW - 1) / NW;
-    // enough blocks to fill 256 CUs several times; strips >= 2T rows keep the
-    // window prologue (T-1+P row loads per strip) a small overhead.
-    int nstrip = (int)((2048LL + (long long)nxb * nkb - 1) / ((long long)nxb * nkb));
-    const int max_strip = H / (2 * T) > 1 ? H / (2 * T) : 1;
-    if (nstrip > max_strip) nstrip = max_strip;
-    if (nstrip < 1) nstrip = 1;
-    const int rows = (H + nstrip - 1) / nstrip;
-    nstrip = (H + rows - 1) / rows;
-    const int per_xcd = (nxb + 7) / 8;
-    const int nblocks = 8 * per_xcd * nkb * nstrip;
-    hipLaunchKernelGGL((k_vpass<T, NW>), dim3(nblocks), dim3(NW * 64), 0, st, wl, wr, cin, cout, W, H, Dp,
-                       p->d_begin, rows, nxb, nstrip, per_xcd);
-}
-
-template <int T, int NW, int XW>
-void launch_h(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
-              hipStream_t st) {
-    const int W = p->width, H = p->height;
-    const int Dp = asw_disp_pitch(p);
-    const int nkb = Dp / 64;
-    constexpr int SEG = NW * XW;
-    const int nseg = (W + SEG - 1) / SEG;
-    const int nblocks = (H * nseg + 7) / 8 * 8 * nkb;
-    hipLaunchKernelGGL((k_hpass<T, NW, XW>), dim3(nblocks), dim3(NW * 64), 0, st, wl, wr, cin, cout, W, H, Dp,
-                       p->d_begin, nseg);
-}
-
 template <int T>
 int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                  hipStream_t st) {
-    constexpr bool kTune = (T == 35);  // extra variants are only built for the benchmark window
-    constexpr int U = T + pf_dist(T);
-    constexpr int XW = U * (64 / U > 1 ? 64 / U : 1);  // a whole number of U-step chunks per sweep
-    const int v = g_pass_variant;
-    if (dir == ASW_DIR_V) {
-        if constexpr (kTune) {
-            if (v & 8) launch_v<T, 8>(p, wl, wr, cin, cout, st);
-            else launch_v<T, 16>(p, wl, wr, cin, cout, st);
-        } else {
-            launch_v<T, 16>(p, wl, wr, cin, cout, st);
-        }
-    } else {
-        if constexpr (kTune) {
-            const int shape = (v >> 1) & 3;
-            if (shape == 1) launch_h<T, 8, XW>(p, wl, wr, cin, cout, st);
-            else if (shape == 2) launch_h<T, 2, 2 * XW>(p, wl, wr, cin, cout, st);
-            else launch_h<T, 4, XW>(p, wl, wr, cin, cout, st);
-        } else {
-            launch_h<T, 4, XW>(p, wl, wr, cin, cout, st);
-        }
-    }
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_hip_error(e);
-        return ASW_E_HIP;
-    }
-    return ASW_OK;
-}
-
-}  // namespace
+                  hipStream_t st);
+}  // namespace agg
 
 int set_pass_variant(int v) {
-    const int old = g_pass_variant;
-    g_pass_variant = v;
+    const int old = agg::g_pass_variant;
+    agg::g_pass_variant = v;
     return old;
 }
 
@@ -378,7 +24,7 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
     switch (p->taps) {
 #define ASW_CASE(TT) \
     case TT:         \
-        return launch_pass_t<TT>(p, dir, wl, wr, cin, cout, st);
+        return agg::launch_pass_t<TT>(p, dir, wl, wr, cin, cout, st);
         ASW_CASE(3)
         ASW_CASE(5)
         ASW_CASE(7)
