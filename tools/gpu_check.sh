@@ -33,4 +33,12 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     python3 bench.py --steps 5 --warmup 1 --no-cpu > "$OUT/prof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc" | tee -a "$OUT/steps.log"; tail -3 "$OUT/prof_$TAG.log"; [ $rc -eq 0 ] || exit $rc
 find "$OUT/prof_$TAG" -name "*stats*" | head
+
+# HBM traffic counters, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit together)
+for c in FETCH_SIZE WRITE_SIZE; do
+  echo "== rocprofv3 --pmc $c" | tee -a "$OUT/steps.log"
+  timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$TAG/$c" -o run -- \
+      python3 bench.py --steps 2 --warmup 1 --no-cpu > "$OUT/pmc_${TAG}_$c.log" 2>&1
+  rc=$?; echo "pmc $c rc=$rc" | tee -a "$OUT/steps.log"; [ $rc -eq 0 ] || { tail -5 "$OUT/pmc_${TAG}_$c.log"; exit $rc; }
+done
 exit 0

@@ -11,7 +11,11 @@ timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 CMD="python3 tools/pass_bench.py --reps 2 --variants $VAR"
 i=0
 SETS=${SETS:-all}
-if [ "$SETS" = "icache" ]; then LIST=(
+if [ "$SETS" = "lat" ]; then LIST=(
+  "SQ_INSTS_LDS SQ_INST_LEVEL_LDS SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
+  "SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SMEM SQ_ACTIVE_INST_SCA SQ_INSTS_VALU SQ_ACTIVE_INST_VALU"
+  "GRBM_GUI_ACTIVE SQ_LEVEL_WAVES SQ_WAVES SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM" )
+elif [ "$SETS" = "icache" ]; then LIST=(
   "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_WAVE_CYCLES"
   "SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_LDS SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" )
 else LIST=(

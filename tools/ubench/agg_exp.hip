@@ -1,0 +1,213 @@
+// Experiment: per-step overheads of the H aggregation pass (v7 structure).
+// Copies of k_hpass (asw_aggregate_impl.h) with parts removed; results are
+// garbage for EXP != 0 (timing only), C4 size.
+//   EXP bit 0: no left-weight scalar loads      bit 1: no right-weight LDS reads
+//   bit 2: keep the weight address arithmetic (sunk into an empty asm)
+//   bit 3: incremental weight addresses (pointer += per step, no clamps)
+#include "../../stereo_matchin_amd/csrc/asw_aggregate_impl.h"
+
+#include <cstdio>
+
+#include <vector>
+
+using namespace asw::agg;
+using asw::tap_pitch;
+
+// taps with the left weights in VGPRs (f4 groups)
+template <int U, int S, int B, int E, int M1, int M2>
+__device__ __forceinline__ void taps_v(float &num, float &den, const f4 (&wl)[M1], const f4 (&wr)[M2],
+                                       const float (&win)[U]) {
+#pragma unroll
+    for (int i = B; i < E; ++i) {
+        const float ww = wl[(i - B) / 4][(i - B) % 4] * wr[(i - B) / 4][(i - B) % 4];
+        num = __builtin_fmaf(ww, win[(S + i) % U], num);
+        den = den + ww;
+    }
+}
+template <int T, int QB, int QE, int M>
+__device__ __forceinline__ void load_wl_v(f4 (&dst)[M], const float *px, int z) {
+#pragma unroll
+    for (int q = QB; q < QE; ++q) dst[q - QB] = reinterpret_cast<const f4 *>(px)[q + z];
+}
+
+template <int T, int NW, int XW, int EXP>
+__global__ __launch_bounds__(NW * 64) void k_hexp(const float *__restrict__ wl, const float *__restrict__ wr,
+                                                   const float *__restrict__ cin, float *__restrict__ cout,
+                                                   int W, int H, int Dp, int d_begin, int nseg) {
+    constexpr int R = T / 2;
+    constexpr int TP = tap_pitch(T);
+    constexpr int Q = TP / 4;
+    constexpr int QT = (T + 3) / 4;
+    constexpr int P = pf_dist(T);
+    constexpr int U = T + P;
+    constexpr int PW = kPW;
+    static_assert(U % PW == 0, "ring period must divide the unroll period");
+    constexpr int SEG = NW * XW;
+    constexpr int SLAB = SEG + 63;
+    constexpr int NQ = SLAB * Q;
+    __shared__ f4 slab[NQ];
+
+    const int nkb = Dp / 64;
+    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int group = (m / nkb) * 8 + xcd;
+    if (group >= H * nseg) return;  // padding block (uniform)
+    const int y = group / nseg;
+    const int xs = (group % nseg) * SEG;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int kb = (m % nkb) * 64;
+    const int k = kb + lane;
+    const int slab_base = xs - (d_begin + kb) - 63;
+
+    const float *wrrow = wr + (long long)y * W * TP;
+    for (int t = threadIdx.x; t < NQ; t += NW * 64) {
+        const int e = t / Q, q = t - e * Q;
+        slab[t] = *reinterpret_cast<const f4 *>(wrrow + clampi(slab_base + e, 0, W - 1) * TP + 4 * q);
+    }
+    __syncthreads();
+
+    const int xw0 = xs + wave * XW;
+    if (xw0 >= W) return;
+    const int xw1 = min(xw0 + XW, W);
+    const float *cbase = cin + (long long)y * W * Dp + k;
+    float *obase = cout + (long long)y * W * Dp + k;
+    const float *wlrow0 = wl + (long long)y * W * TP;
+    const f4 *my_slab = &slab[(63 - lane) * Q];
+    const int warm_off = lane < TP ? lane : 0;
+
+    using HV = Halves<T>;
+    float win[U];
+    float warm[PW];
+    float sink = 0.0f;
+    float wla[HV::NA], wlb[HV::NB];
+    f4 wra[HV::MA], wrb[HV::MB];
+    f4 wlva[HV::MA], wlvb[HV::MB];
+    int zv;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
+#pragma unroll
+    for (int j = 0; j < T - 1 + P; ++j) win[j] = cbase[(long long)clampi(xw0 - R + j, 0, W - 1) * Dp];
+#pragma unroll
+    for (int j = 0; j < PW; ++j) warm[j] = wlrow0[clampi(xw0 + j, 0, W - 1) * TP + warm_off];
+    load_wl<0, HV::TA>(wla, wlrow0 + xw0 * TP);
+    if constexpr ((EXP & 16) != 0) load_wl_v<T, 0, HV::QA>(wlva, wlrow0 + xw0 * TP, zv);
+    read_wr<T, 0, HV::QA>(wra, my_slab + (xw0 - xs) * Q);
+    if constexpr (HV::TB > 0) {  // initialised for the variants that never reload them
+        load_wl<HV::TA, T>(wlb, wlrow0 + xw0 * TP);
+        read_wr<T, HV::QA, HV::QT>(wrb, my_slab + (xw0 - xs) * Q);
+        if constexpr ((EXP & 16) != 0) load_wl_v<T, HV::QA, HV::QT>(wlvb, wlrow0 + xw0 * TP, zv);
+    }
+
+    const float *wlx = wlrow0 + xw0 * TP;
+    const f4 *wrx = my_slab + (xw0 - xs) * Q;
+    auto body = [&](auto sc, auto chk, int xb) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc)::value;
+        int x = xb + s;
+        asm volatile("" : "+s"(x));  // opaque per step (see the V pass)
+        if constexpr (decltype(chk)::value) {
+            if (x >= xw1) return;
+        }
+        wait_lgkm0();  // half A's weights
+        __builtin_amdgcn_sched_barrier(0);
+        const float *pwl = (EXP & 8) ? wlx : wlrow0 + x * TP;
+        const f4 *pwr = (EXP & 8) ? wrx : my_slab + (x - xs) * Q;
+        if constexpr (HV::TB > 0) {
+            if constexpr ((EXP & 16) != 0) load_wl_v<T, HV::QA, HV::QT>(wlvb, pwl, zv);
+            else if constexpr (!(EXP & 1)) load_wl<HV::TA, T>(wlb, pwl);
+            if constexpr (!(EXP & 2)) read_wr<T, HV::QA, HV::QT>(wrb, pwr);
+            if constexpr ((EXP & 4) != 0) asm volatile("" ::"s"(pwl), "v"(pwr));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        float num = 1e-5f, den = 1e-5f;
+        if constexpr ((EXP & 16) != 0) taps_v<U, s, 0, HV::TA>(num, den, wlva, wra, win);
+        else taps<U, s, 0, HV::TA>(num, den, wla, wra, win);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_lgkm0();  // half B's weights
+        __builtin_amdgcn_sched_barrier(0);
+        const int xn = min(x + 1, xw1 - 1);
+        if constexpr ((EXP & 8) != 0) { wlx += TP; wrx += Q; }
+        const float *qwl = (EXP & 8) ? wlx : wlrow0 + xn * TP;
+        const f4 *qwr = (EXP & 8) ? wrx : my_slab + (xn - xs) * Q;
+        if constexpr ((EXP & 16) != 0) load_wl_v<T, 0, HV::QA>(wlva, qwl, zv);
+        else if constexpr (!(EXP & 1)) load_wl<0, HV::TA>(wla, qwl);
+        if constexpr (!(EXP & 2)) read_wr<T, 0, HV::QA>(wra, qwr);
+        if constexpr ((EXP & 4) != 0) asm volatile("" ::"s"(qwl), "v"(qwr));
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((EXP & 16) != 0) taps_v<U, s, HV::TA, T>(num, den, wlvb, wrb, win);
+        else if constexpr (HV::TB > 0) taps<U, s, HV::TA, T>(num, den, wlb, wrb, win);
+        obase[(long long)x * Dp] = div_pos(num, den);
+        win[(s + U - 1) % U] = cbase[(long long)clampi(x + R + P, 0, W - 1) * Dp];
+        sink += warm[s % PW];
+        warm[s % PW] = wlrow0[clampi(x + PW, 0, W - 1) * TP + warm_off];
+    };
+    int xb = xw0;
+    for (; xb + U <= xw1; xb += U)
+        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::false_type{}, xb); });
+    if (xb < xw1)
+        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::true_type{}, xb); });
+    if (sink == -1.0f) cout[k] = sink;  // never true (weights > 0): keeps the warm loads
+}
+
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            return 1;                                                           \
+        }                                                                       \
+    } while (0)
+
+template <int EXP>
+float run(const float *wl, const float *wr, const float *cin, float *cout, int W, int H, int Dp, int reps) {
+    constexpr int T = 35, NW = 4;
+    constexpr int U = T + pf_dist(T);
+    constexpr int XW = U * (64 / U > 1 ? 64 / U : 1);
+    const int nseg = (W + NW * XW - 1) / (NW * XW);
+    const int nblocks = (H * nseg + 7) / 8 * 8 * (Dp / 64);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    hipLaunchKernelGGL((k_hexp<T, NW, XW, EXP>), dim3(nblocks), dim3(NW * 64), 0, 0, wl, wr, cin, cout, W, H, Dp, 0, nseg);
+    (void)hipEventRecord(a);
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL((k_hexp<T, NW, XW, EXP>), dim3(nblocks), dim3(NW * 64), 0, 0, wl, wr, cin, cout, W, H, Dp, 0,
+                           nseg);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms;
+    (void)hipEventElapsedTime(&ms, a, b);
+    return ms / reps;
+}
+
+int main() {
+    const int W = 1920, H = 1080, Dp = 256, TP = tap_pitch(35);
+    const size_t nc = (size_t)W * H * Dp, ns = (size_t)W * H * TP;
+    float *wl, *wr, *cin, *cout;
+    CK(hipMalloc(&wl, ns * 4));
+    CK(hipMalloc(&wr, ns * 4));
+    CK(hipMalloc(&cin, nc * 4));
+    CK(hipMalloc(&cout, nc * 4));
+    std::vector<float> h(ns);
+    for (size_t i = 0; i < ns; ++i) h[i] = 0.1f + (float)((i * 2654435761u) % 1000) * 1e-3f;
+    CK(hipMemcpy(wl, h.data(), ns * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(wr, h.data(), ns * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(cin, 0x3f, nc * 4));
+    const double bytes = 8.0 * 256 * W * H + 8.0 * 35 * W * H;
+    const int exps[] = {0, 1, 2, 3, 7, 16};
+    const char *names[] = {"full", "no SMEM", "no LDS reads", "no weight loads", "no weight loads, keep address math",
+                           "left weights by uniform vector loads"};
+    float ms[6];
+    for (int rep = 0; rep < 2; ++rep) {
+        ms[0] = run<0>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[1] = run<1>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[2] = run<2>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[3] = run<3>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[4] = run<7>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[5] = run<16>(wl, wr, cin, cout, W, H, Dp, 10);
+    }
+    CK(hipGetLastError());
+    for (int e = 0; e < 6; ++e)
+        printf("{\"exp\": %d, \"what\": \"%s\", \"ms\": %.4f, \"alg_GBps\": %.1f}\n", exps[e], names[e], ms[e],
+               bytes / ms[e] / 1e6);
+    return 0;
+}
