@@ -43,7 +43,7 @@ extern "C" {
 #define ASW_DIR_H 1 /* horizontal pass / support (asw_hSupport, asw_hCostAggregation) */
 
 #define ASW_COLOR_RGB 0 /* reference: RGB sum of absolute differences (K/asw_vsupport.cl:22) */
-#define ASW_COLOR_LAB 1 /* extension (north star): CIELab Euclidean distance, unpinned       */
+#define ASW_COLOR_LAB 1 /* extension (north star): CIELab Euclidean distance (asw_lab)     */
 
 #define ASW_LR_U8 0     /* parity: compare 8-bit codes like K/consist.cl:20-30 */
 #define ASW_LR_NATIVE 1 /* |d_ref - d_tar| <= 1 on integer indices (D > 256)   */
@@ -78,6 +78,7 @@ int asw_tap_pitch(const asw_params *p);  /* Tp = smallest 4k >= taps with k odd 
 size_t asw_cost_bytes(const asw_params *p);    /* H*W*Dp*4   */
 size_t asw_support_bytes(const asw_params *p); /* H*W*Tp*4   */
 size_t asw_lut_bytes(const asw_params *p);     /* (R+1)*766*4 */
+size_t asw_lab_bytes(const asw_params *p);     /* H*W*16 (float4 per pixel) */
 
 /* ---------------- STAGE API (device pointers, async on `stream`) ---------------- */
 
@@ -91,9 +92,20 @@ int asw_raw_cost(const asw_params *p, const uint8_t *left_rgba, const uint8_t *r
 int asw_support_lut(const asw_params *p, float *lut, void *stream);
 
 /* replaces asw_vSupport / asw_hSupport (K/asw_vsupport.cl:3-27, K/asw_hsupport.cl:3-28),
- * launched at main.cpp:469-484 (once per image and direction). */
+ * launched at main.cpp:469-484 (once per image and direction).  RGB contexts only
+ * (ASW_E_INVALID for ASW_COLOR_LAB: use asw_lab + asw_support_lab). */
 int asw_support(const asw_params *p, int dir, const uint8_t *img_rgba, const float *lut, float *w,
                 void *stream);
+
+/* CIELab extension (north star; the reference has no colour conversion, so this
+ * is not reference-pinned: the oracle restates the same IEEE double sequence and
+ * colorimetric known answers pin the conversion).  With p->color_space ==
+ * ASW_COLOR_LAB the support weights use the Euclidean L*a*b* distance in place of
+ * the RGB SAD of K/asw_vsupport.cl:19-25; the raw cost stays RGB AD/TAD.
+ *   asw_lab:          lab[y][x] = (L*, a*, b*, 0) float4 of an RGBA8 image (sRGB, D65)
+ *   asw_support_lab:  the asw_support of a LAB context, from a lab image. */
+int asw_lab(const asw_params *p, const uint8_t *img_rgba, float *lab, void *stream);
+int asw_support_lab(const asw_params *p, int dir, const float *lab, float *w, void *stream);
 
 /* replaces asw_vCostAggregation / asw_hCostAggregation (K/asw_vcost_aggregation.cl:11-44,
  * K/asw_hcost_aggregation.cl:12-44), launched at main.cpp:494-509.  One pass over

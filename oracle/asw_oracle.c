@@ -26,6 +26,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include "srgb_table.h"
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -40,7 +42,7 @@
 
 static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-int oracle_version(void) { return 3; }
+int oracle_version(void) { return 4; }
 
 int oracle_set_threads(int n) {
 #ifdef _OPENMP
@@ -251,12 +253,88 @@ void oracle_consistency(const uint8_t *code_ref, const uint8_t *code_tar, float 
     }
 }
 
+/* Truncated AD (north-star extension): min(tau, AD) with the AD of
+ * oracle_raw_cost; tau >= 765 is the reference's plain AD. */
+void oracle_raw_cost_tad(const uint8_t *L, const uint8_t *R, int W, int H, int D, float tau, float *C) {
+    const long S = (long)W * H;
+    oracle_raw_cost(L, R, W, H, D, C);
+    if (tau >= 765.0f) return;
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < S * D; ++i) C[i] = fminf(C[i], tau);
+}
+
+/* ---- CIELab extension (north star, no reference counterpart) ----
+ * sRGB (D65) 8-bit -> CIE L*a*b*.  Linear light from the shared generated table
+ * (srgb_table.h), XYZ by the IEC 61966-2-1 matrix, white (0.95047, 1, 1.08883),
+ * f(t) = cbrt(t) above (6/29)^3 else (kappa t + 16)/116, kappa = 24389/27.
+ * A fixed sequence of IEEE double operations (no libm): the cube root is 12
+ * Newton steps from 1.0, so the HIP kernel reproduces it bit for bit.  Results
+ * are rounded to float. */
+static double cbrt_newton(double t) {
+    double y = 1.0;
+    for (int k = 0; k < 12; ++k) y = (2.0 * y + t / (y * y)) / 3.0;
+    return y;
+}
+
+static double lab_f(double t) {
+    const double eps = 216.0 / 24389.0, kappa = 24389.0 / 27.0;
+    return t > eps ? cbrt_newton(t) : (kappa * t + 16.0) / 116.0;
+}
+
+void oracle_lab(const uint8_t *img, int W, int H, float *lab) {
+    const long S = (long)W * H;
+#pragma omp parallel for schedule(static)
+    for (long p = 0; p < S; ++p) {
+        const double r = SRGB_LINEAR[img[4 * p]], g = SRGB_LINEAR[img[4 * p + 1]], b = SRGB_LINEAR[img[4 * p + 2]];
+        const double X = (0.4124564 * r + 0.3575761 * g) + 0.1804375 * b;
+        const double Y = (0.2126729 * r + 0.7151522 * g) + 0.0721750 * b;
+        const double Z = (0.0193339 * r + 0.1191920 * g) + 0.9503041 * b;
+        const double fx = lab_f(X / 0.95047), fy = lab_f(Y / 1.0), fz = lab_f(Z / 1.08883);
+        lab[4 * p] = (float)(116.0 * fy - 16.0);
+        lab[4 * p + 1] = (float)(500.0 * (fx - fy));
+        lab[4 * p + 2] = (float)(200.0 * (fy - fz));
+        lab[4 * p + 3] = 0.0f;
+    }
+}
+
+/* Support weights with the colour term on CIELab: the reference formula of
+ * K/asw_vsupport.cl:19-25 with the RGB SAD replaced by the Euclidean Lab
+ * distance dc = sqrt((dL^2 + da^2) + db^2) (float sums, double sqrt rounded to
+ * float = the correctly rounded float sqrt). */
+float oracle_support_weight_lab(const float *lp, const float *lq, int dist, float gamma_c, float gamma_g) {
+    const float dL = lp[0] - lq[0], da = lp[1] - lq[1], db = lp[2] - lq[2];
+    float s = dL * dL + da * da;
+    s = s + db * db;
+    const float dc = (float)sqrt((double)s);
+    const float c_diff = (-dc) / gamma_c;
+    const float g_dist = (float)dist / gamma_g;
+    return (float)exp((double)(c_diff - g_dist));
+}
+
+void oracle_support_lab(const float *lab, int W, int H, int T, int dir, float gamma_c, float gamma_g, float *out) {
+    const int Rr = T / 2;
+    const long S = (long)W * H;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y) {
+        for (int i = 0; i < T; ++i) {
+            for (int x = 0; x < W; ++x) {
+                int qx = x, qy = y;
+                if (dir == 0) qy = clampi(y + i - Rr, 0, H - 1);
+                else qx = clampi(x + i - Rr, 0, W - 1);
+                const int dist = dir == 0 ? abs(y - qy) : abs(x - qx);
+                out[(long)i * S + (long)y * W + x] = oracle_support_weight_lab(
+                    lab + 4 * ((long)y * W + x), lab + 4 * ((long)qy * W + qx), dist, gamma_c, gamma_g);
+            }
+        }
+    }
+}
+
 /* main.cpp:463-537 — raw cost, 4 support launches, r x (V,H), WTA, consistency.
  * Scratch is allocated here.  Outputs may be NULL when not wanted.
  * cost_out (if not NULL) receives the final aggregated volume [D][H][W]. */
-int oracle_match(const uint8_t *L, const uint8_t *R, int W, int H, int D, int T, int iters, float gamma_c,
-                 float gamma_g, int fma_mode, int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar,
-                 uint8_t *out_rgba, uint8_t *out_red_rgba, float *cost_out) {
+int oracle_match_ex(const uint8_t *L, const uint8_t *R, int W, int H, int D, int T, int iters, float gamma_c,
+                    float gamma_g, int fma_mode, int color_space, float tad_tau, int32_t *d_ref, float *conf_ref,
+                    int32_t *d_tar, float *conf_tar, uint8_t *out_rgba, uint8_t *out_red_rgba, float *cost_out) {
     const long S = (long)W * H;
     float *c0 = (float *)malloc(sizeof(float) * S * D);
     float *c1 = (float *)malloc(sizeof(float) * S * D);
@@ -271,11 +349,24 @@ int oracle_match(const uint8_t *L, const uint8_t *R, int W, int H, int D, int T,
     uint8_t *kr = (uint8_t *)malloc(S), *kt = (uint8_t *)malloc(S);
     uint8_t *o1 = (uint8_t *)malloc(4 * S), *o2 = (uint8_t *)malloc(4 * S);
     if (!c0 || !c1 || !vl || !vr || !hl || !hr || !dr || !dt || !cr || !ct || !kr || !kt || !o1 || !o2) return -1;
-    oracle_raw_cost(L, R, W, H, D, c0);
-    oracle_support(L, W, H, T, 0, gamma_c, gamma_g, vl);
-    oracle_support(L, W, H, T, 1, gamma_c, gamma_g, hl);
-    oracle_support(R, W, H, T, 0, gamma_c, gamma_g, vr);
-    oracle_support(R, W, H, T, 1, gamma_c, gamma_g, hr);
+    oracle_raw_cost_tad(L, R, W, H, D, tad_tau, c0);
+    if (color_space == 1) {
+        float *labL = (float *)malloc(sizeof(float) * 4 * S), *labR = (float *)malloc(sizeof(float) * 4 * S);
+        if (!labL || !labR) return -1;
+        oracle_lab(L, W, H, labL);
+        oracle_lab(R, W, H, labR);
+        oracle_support_lab(labL, W, H, T, 0, gamma_c, gamma_g, vl);
+        oracle_support_lab(labL, W, H, T, 1, gamma_c, gamma_g, hl);
+        oracle_support_lab(labR, W, H, T, 0, gamma_c, gamma_g, vr);
+        oracle_support_lab(labR, W, H, T, 1, gamma_c, gamma_g, hr);
+        free(labL);
+        free(labR);
+    } else {
+        oracle_support(L, W, H, T, 0, gamma_c, gamma_g, vl);
+        oracle_support(L, W, H, T, 1, gamma_c, gamma_g, hl);
+        oracle_support(R, W, H, T, 0, gamma_c, gamma_g, vr);
+        oracle_support(R, W, H, T, 1, gamma_c, gamma_g, hr);
+    }
     for (int it = 0; it < iters; ++it) {
         oracle_pass(vl, vr, c0, c1, W, H, T, 0, 0, D, 0, fma_mode); /* V: c0 -> c1 */
         oracle_pass(hl, hr, c1, c0, W, H, T, 1, 0, D, 0, fma_mode); /* H: c1 -> c0 */
@@ -296,4 +387,12 @@ int oracle_match(const uint8_t *L, const uint8_t *R, int W, int H, int D, int T,
     free(c0); free(c1); free(vl); free(vr); free(hl); free(hr);
     free(dr); free(dt); free(cr); free(ct); free(kr); free(kt); free(o1); free(o2);
     return 0;
+}
+
+/* the reference configuration: RGB colour term, plain AD */
+int oracle_match(const uint8_t *L, const uint8_t *R, int W, int H, int D, int T, int iters, float gamma_c,
+                 float gamma_g, int fma_mode, int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar,
+                 uint8_t *out_rgba, uint8_t *out_red_rgba, float *cost_out) {
+    return oracle_match_ex(L, R, W, H, D, T, iters, gamma_c, gamma_g, fma_mode, 0, 765.0f, d_ref, conf_ref, d_tar,
+                           conf_tar, out_rgba, out_red_rgba, cost_out);
 }

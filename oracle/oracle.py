@@ -71,6 +71,11 @@ def lib():
     L.oracle_consistency.argtypes = [P, P, P, P, i, i, i, P, P]
     L.oracle_match.argtypes = [P, P, i, i, i, i, i, f, f, i, P, P, P, P, P, P, P]
     L.oracle_match.restype = i
+    L.oracle_match_ex.argtypes = [P, P, i, i, i, i, i, f, f, i, i, f, P, P, P, P, P, P, P]
+    L.oracle_match_ex.restype = i
+    L.oracle_raw_cost_tad.argtypes = [P, P, i, i, i, f, P]
+    L.oracle_lab.argtypes = [P, i, i, P]
+    L.oracle_support_lab.argtypes = [P, i, i, i, i, f, f, P]
     _lib = L
     return L
 
@@ -99,6 +104,29 @@ def support(img: np.ndarray, T: int, direction: int, gc: float = GAMMA_C, gg: fl
     H, W = img.shape[:2]
     out = np.empty((T, H, W), np.float32)
     lib().oracle_support(_p(img), W, H, T, direction, gc, gg, _p(out))
+    return out
+
+
+def raw_cost_tad(L: np.ndarray, R: np.ndarray, D: int, tau: float) -> np.ndarray:
+    H, W = L.shape[:2]
+    C = np.empty((D, H, W), np.float32)
+    lib().oracle_raw_cost_tad(_p(L), _p(R), W, H, D, tau, _p(C))
+    return C
+
+
+def lab(img: np.ndarray) -> np.ndarray:
+    """CIELab (D65) of an RGBA8 image: float32 [H][W][4] = (L*, a*, b*, 0)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape[:2]
+    out = np.empty((H, W, 4), np.float32)
+    lib().oracle_lab(_p(img), W, H, _p(out))
+    return out
+
+
+def support_lab(lab_img: np.ndarray, T: int, direction: int, gc: float = GAMMA_C, gg: float = GAMMA_G):
+    H, W = lab_img.shape[:2]
+    out = np.empty((T, H, W), np.float32)
+    lib().oracle_support_lab(_p(np.ascontiguousarray(lab_img, np.float32)), W, H, T, direction, gc, gg, _p(out))
     return out
 
 
@@ -142,7 +170,8 @@ def consistency(code_ref, code_tar, conf_ref, conf_tar, D: int):
 
 
 def match(L: np.ndarray, R: np.ndarray, D: int, T: int, iters: int = 7, gc: float = GAMMA_C,
-          gg: float = GAMMA_G, fma_mode: int = FMA_NUM, want_cost: bool = False) -> dict:
+          gg: float = GAMMA_G, fma_mode: int = FMA_NUM, want_cost: bool = False, color_space: int = 0,
+          tad_tau: float = 765.0) -> dict:
     """Full reference ASW pipeline (main.cpp:463-537) on host RGBA8 images [H][W][4]."""
     L = np.ascontiguousarray(L, np.uint8)
     R = np.ascontiguousarray(R, np.uint8)
@@ -153,7 +182,7 @@ def match(L: np.ndarray, R: np.ndarray, D: int, T: int, iters: int = 7, gc: floa
         "lr_rgba": np.empty((H, W, 4), np.uint8), "lr_red_rgba": np.empty((H, W, 4), np.uint8),
     }
     cost = np.empty((D, H, W), np.float32) if want_cost else None
-    rc = lib().oracle_match(_p(L), _p(R), W, H, D, T, iters, gc, gg, fma_mode,
+    rc = lib().oracle_match_ex(_p(L), _p(R), W, H, D, T, iters, gc, gg, fma_mode, color_space, tad_tau,
                             _p(out["d_ref"]), _p(out["conf_ref"]), _p(out["d_tar"]), _p(out["conf_tar"]),
                             _p(out["lr_rgba"]), _p(out["lr_red_rgba"]),
                             _p(cost) if cost is not None else None)

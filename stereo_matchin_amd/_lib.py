@@ -110,6 +110,9 @@ SIGNATURES = {
     "asw_raw_cost": (I, [PP, P, P, P, P]),
     "asw_support_lut": (I, [PP, P, P]),
     "asw_support": (I, [PP, I, P, P, P, P]),
+    "asw_lab_bytes": (ctypes.c_size_t, [PP]),
+    "asw_lab": (I, [PP, P, P, P]),
+    "asw_support_lab": (I, [PP, I, P, P, P]),
     "asw_aggregate_pass": (I, [PP, I, P, P, P, P, P]),
     "asw_aggregate": (I, [PP, P, P, P, P, P, P, P]),
     "asw_wta": (I, [PP, P, P, P, P, P, P, P, P]),

@@ -18,6 +18,7 @@ struct asw_ctx {
     hipStream_t stream = nullptr;
     uint8_t *left = nullptr, *right = nullptr;  // RGBA8 [H][W][4]
     float *lut = nullptr;
+    float *lab_l = nullptr, *lab_r = nullptr;  // float4 [H][W] (ASW_COLOR_LAB only)
     float *wvl = nullptr, *wvr = nullptr, *whl = nullptr, *whr = nullptr;  // [H][W][Tp]
     float *c0 = nullptr, *c1 = nullptr;                                    // [H][W][Dp]
     int32_t *d_ref = nullptr, *d_tar = nullptr;
@@ -76,7 +77,7 @@ extern "C" {
 int asw_destroy(asw_ctx *ctx) {
     if (!ctx) return ASW_OK;
     (void)hipSetDevice(ctx->device);
-    void *bufs[] = {ctx->left, ctx->right, ctx->lut, ctx->wvl, ctx->wvr, ctx->whl, ctx->whr, ctx->c0, ctx->c1,
+    void *bufs[] = {ctx->left, ctx->right, ctx->lut, ctx->lab_l, ctx->lab_r, ctx->wvl, ctx->wvr, ctx->whl, ctx->whr, ctx->c0, ctx->c1,
                     ctx->d_ref, ctx->d_tar, ctx->conf_ref, ctx->conf_tar, ctx->code_ref, ctx->code_tar, ctx->lr,
                     ctx->lr_red, ctx->disp};
     for (void *b : bufs)
@@ -112,6 +113,10 @@ int asw_create(const asw_params *p, int hip_device, asw_ctx **out) {
     chain(dev_alloc(&c->left, S * 4));
     chain(dev_alloc(&c->right, S * 4));
     chain(dev_alloc(&c->lut, asw_lut_bytes(p)));
+    if (p->color_space == ASW_COLOR_LAB) {
+        chain(dev_alloc(&c->lab_l, asw_lab_bytes(p)));
+        chain(dev_alloc(&c->lab_r, asw_lab_bytes(p)));
+    }
     chain(dev_alloc(&c->wvl, asw_support_bytes(p)));
     chain(dev_alloc(&c->wvr, asw_support_bytes(p)));
     chain(dev_alloc(&c->whl, asw_support_bytes(p)));
@@ -156,11 +161,20 @@ int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
     HIPCHK(hipEventRecord(ev[1], st));
     ASWCHK(asw_raw_cost(p, c->left, c->right, c->c0, st));
     HIPCHK(hipEventRecord(ev[2], st));
-    ASWCHK(asw_support_lut(p, c->lut, st));
-    ASWCHK(asw_support(p, ASW_DIR_V, c->left, c->lut, c->wvl, st));
-    ASWCHK(asw_support(p, ASW_DIR_H, c->left, c->lut, c->whl, st));
-    ASWCHK(asw_support(p, ASW_DIR_V, c->right, c->lut, c->wvr, st));
-    ASWCHK(asw_support(p, ASW_DIR_H, c->right, c->lut, c->whr, st));
+    if (p->color_space == ASW_COLOR_LAB) {
+        ASWCHK(asw_lab(p, c->left, c->lab_l, st));
+        ASWCHK(asw_lab(p, c->right, c->lab_r, st));
+        ASWCHK(asw_support_lab(p, ASW_DIR_V, c->lab_l, c->wvl, st));
+        ASWCHK(asw_support_lab(p, ASW_DIR_H, c->lab_l, c->whl, st));
+        ASWCHK(asw_support_lab(p, ASW_DIR_V, c->lab_r, c->wvr, st));
+        ASWCHK(asw_support_lab(p, ASW_DIR_H, c->lab_r, c->whr, st));
+    } else {
+        ASWCHK(asw_support_lut(p, c->lut, st));
+        ASWCHK(asw_support(p, ASW_DIR_V, c->left, c->lut, c->wvl, st));
+        ASWCHK(asw_support(p, ASW_DIR_H, c->left, c->lut, c->whl, st));
+        ASWCHK(asw_support(p, ASW_DIR_V, c->right, c->lut, c->wvr, st));
+        ASWCHK(asw_support(p, ASW_DIR_H, c->right, c->lut, c->whr, st));
+    }
     HIPCHK(hipEventRecord(ev[3], st));
     if (timed) HIPCHK(hipEventRecord(ev[e_pass0], st));
     for (int it = 0; it < r; ++it) {

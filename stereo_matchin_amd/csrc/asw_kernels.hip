@@ -21,6 +21,7 @@
 #include <cstdint>
 
 #include "asw_common.h"
+#include "asw_srgb_table.h"
 
 namespace asw {
 
@@ -127,6 +128,75 @@ __global__ void k_support(const uchar4 *__restrict__ img, const float *__restric
             const uchar4 b = img[(long long)qy * W + qx];
             const int sad = abs((int)a.x - (int)b.x) + abs((int)a.y - (int)b.y) + abs((int)a.z - (int)b.z);
             v = lut[dist * kLutWidth + sad];
+        }
+        w[idx] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CIELab extension (north star, no reference counterpart).
+// sRGB (D65) 8-bit -> L*a*b*: linear light from the generated table
+// (asw_srgb_table.h), the IEC 61966-2-1 matrix, white (0.95047, 1, 1.08883),
+// f(t) = cbrt(t) above (6/29)^3 else (kappa t + 16)/116.  A fixed sequence of
+// IEEE double operations (the cube root is 12 Newton steps from 1.0, no libm),
+// compiled with -ffp-contract=off: identical to oracle_lab bit for bit.
+// ---------------------------------------------------------------------------
+__device__ double cbrt_newton(double t) {
+    double y = 1.0;
+#pragma unroll 1
+    for (int k = 0; k < 12; ++k) y = (2.0 * y + t / (y * y)) / 3.0;
+    return y;
+}
+
+__device__ double lab_f(double t) {
+    const double eps = 216.0 / 24389.0, kappa = 24389.0 / 27.0;
+    return t > eps ? cbrt_newton(t) : (kappa * t + 16.0) / 116.0;
+}
+
+__global__ void k_lab(const uchar4 *__restrict__ img, float4 *__restrict__ lab, long long n) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uchar4 c = img[p];
+    const double r = kSrgbLinear[c.x], g = kSrgbLinear[c.y], b = kSrgbLinear[c.z];
+    const double X = (0.4124564 * r + 0.3575761 * g) + 0.1804375 * b;
+    const double Y = (0.2126729 * r + 0.7151522 * g) + 0.0721750 * b;
+    const double Z = (0.0193339 * r + 0.1191920 * g) + 0.9503041 * b;
+    const double fx = lab_f(X / 0.95047), fy = lab_f(Y / 1.0), fz = lab_f(Z / 1.08883);
+    lab[p] = make_float4((float)(116.0 * fy - 16.0), (float)(500.0 * (fx - fy)), (float)(200.0 * (fy - fz)), 0.0f);
+}
+
+// Support weights with the colour term on CIELab: the formula of
+// K/asw_vsupport.cl:19-25 with the RGB SAD replaced by the Euclidean distance
+// dc = sqrt((dL^2 + da^2) + db^2) (float sums; the double sqrt rounded to float
+// is the correctly rounded float sqrt), exp as exp_d.
+__global__ void k_support_lab(const float4 *__restrict__ lab, float *__restrict__ w, int W, int H, int T, int Tp,
+                              int dir, float gamma_c, float gamma_g) {
+    const long long n = (long long)W * H * Tp;
+    const int R = T / 2;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int i = (int)(idx % Tp);
+        const long long p = idx / Tp;
+        float v = 0.0f;
+        if (i < T) {
+            const int x = (int)(p % W), y = (int)(p / W);
+            int qx = x, qy = y, dist;
+            if (dir == ASW_DIR_V) {
+                qy = clampi(y + i - R, 0, H - 1);
+                dist = y > qy ? y - qy : qy - y;
+            } else {
+                qx = clampi(x + i - R, 0, W - 1);
+                dist = x > qx ? x - qx : qx - x;
+            }
+            const float4 a = lab[p];
+            const float4 b = lab[(long long)qy * W + qx];
+            const float dL = a.x - b.x, da = a.y - b.y, db = a.z - b.z;
+            float s2 = dL * dL + da * da;
+            s2 = s2 + db * db;
+            const float dc = (float)sqrt((double)s2);
+            const float c_diff = (-dc) / gamma_c;
+            const float g_dist = (float)dist / gamma_g;
+            v = (float)exp_d((double)(c_diff - g_dist));
         }
         w[idx] = v;
     }
@@ -381,7 +451,7 @@ int asw_params_check(const asw_params *p) {
     if (p->width < 1 || p->height < 1 || p->ndisp < 1 || p->taps < 1 || (p->taps & 1) == 0) return ASW_E_INVALID;
     if (p->iters < 0 || !(p->gamma_c > 0.0f) || !(p->gamma_g > 0.0f)) return ASW_E_INVALID;
     if (p->d_begin < 0 || d_end_of(p) > p->ndisp || p->d_begin >= d_end_of(p)) return ASW_E_INVALID;
-    if (p->color_space != ASW_COLOR_RGB) return ASW_E_UNSUPPORTED;
+    if (p->color_space != ASW_COLOR_RGB && p->color_space != ASW_COLOR_LAB) return ASW_E_INVALID;
     if (p->lr_mode != ASW_LR_U8 && p->lr_mode != ASW_LR_NATIVE) return ASW_E_INVALID;
     if ((long long)p->width * p->height > (1LL << 31) / 64) return ASW_E_INVALID;
     return ASW_OK;
@@ -408,6 +478,8 @@ size_t asw_cost_bytes(const asw_params *p) {
 size_t asw_support_bytes(const asw_params *p) {
     return (size_t)p->width * p->height * (size_t)asw_tap_pitch(p) * sizeof(float);
 }
+size_t asw_lab_bytes(const asw_params *p) { return p ? (size_t)p->width * p->height * 16 : 0; }
+
 size_t asw_lut_bytes(const asw_params *p) { return (size_t)(p->taps / 2 + 1) * kLutWidth * sizeof(float); }
 
 // ===========================================================================
@@ -442,10 +514,32 @@ int asw_support_lut(const asw_params *p, float *lut, void *stream) {
 int asw_support(const asw_params *p, int dir, const uint8_t *img, const float *lut, float *w, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!img || !lut || !w || (dir != ASW_DIR_V && dir != ASW_DIR_H)) return ASW_E_INVALID;
+    if (p->color_space != ASW_COLOR_RGB) return ASW_E_INVALID;  // LAB contexts: asw_support_lab
     const int Tp = asw_tap_pitch(p);
     const long long n = (long long)p->width * p->height * Tp;
     hipLaunchKernelGGL(k_support, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const uchar4 *>(img), lut, w, p->width, p->height, p->taps, Tp, dir);
+    return finish_launch();
+}
+
+int asw_lab(const asw_params *p, const uint8_t *img, float *lab, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!img || !lab) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    hipLaunchKernelGGL(k_lab, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uchar4 *>(img), reinterpret_cast<float4 *>(lab), n);
+    return finish_launch();
+}
+
+int asw_support_lab(const asw_params *p, int dir, const float *lab, float *w, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!lab || !w || (dir != ASW_DIR_V && dir != ASW_DIR_H)) return ASW_E_INVALID;
+    if (p->color_space != ASW_COLOR_LAB) return ASW_E_INVALID;
+    const int Tp = asw_tap_pitch(p);
+    const long long n = (long long)p->width * p->height * Tp;
+    hipLaunchKernelGGL(k_support_lab, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4 *>(lab), w, p->width, p->height, p->taps, Tp, dir, p->gamma_c,
+                       p->gamma_g);
     return finish_launch();
 }
 

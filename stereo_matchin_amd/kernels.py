@@ -105,6 +105,27 @@ def _support(p: AswParams, direction: int, img: torch.Tensor, lut: torch.Tensor 
     return out
 
 
+def lab_image(p: AswParams, img: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """CIELab (D65) of an RGBA8 image, float32 [H][W][4] = (L*, a*, b*, 0) (north-star extension)."""
+    _expect(img, (p.height, p.width, 4), torch.uint8, "image")
+    if out is None:
+        out = torch.empty((p.height, p.width, 4), dtype=torch.float32, device=img.device)
+    _expect(out, (p.height, p.width, 4), torch.float32, "out")
+    _lib.check(_lib.lib().asw_lab(ctypes.byref(p), _ptr(img), _ptr(out), _stream(img.device)), "asw_lab")
+    return out
+
+
+def support_lab(p: AswParams, direction: int, lab: torch.Tensor, out=None) -> torch.Tensor:
+    """Support weights of a CIELab context (Euclidean L*a*b* colour term)."""
+    _expect(lab, (p.height, p.width, 4), torch.float32, "lab")
+    if out is None:
+        out = new_support(p, lab.device)
+    _expect(out, support_shape(p), torch.float32, "out")
+    _lib.check(_lib.lib().asw_support_lab(ctypes.byref(p), direction, _ptr(lab), _ptr(out), _stream(lab.device)),
+               "asw_support_lab")
+    return out
+
+
 def asw_vSupport(p: AswParams, img: torch.Tensor, lut: torch.Tensor | None = None, out=None):
     """Vertical support weights (K/asw_vsupport.cl:3-27)."""
     return _support(p, DIR_V, img, lut, out)

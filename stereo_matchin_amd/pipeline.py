@@ -20,7 +20,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
-from ._lib import AswParams
+from ._lib import COLOR_LAB, DIR_H, DIR_V, AswParams
 
 
 def make_params(width: int, height: int, ndisp: int = 61, taps: int = 33, iters: int = 7, **kw) -> AswParams:
@@ -61,6 +61,13 @@ class StereoMatcher:
     def raw_and_support(self, left: torch.Tensor, right: torch.Tensor):
         p = self.p
         K.asw_Aggr(p, left, right, out=self.c0)
+        if p.color_space == COLOR_LAB:
+            lab_l, lab_r = K.lab_image(p, left), K.lab_image(p, right)
+            K.support_lab(p, DIR_V, lab_l, out=self.wvl)
+            K.support_lab(p, DIR_H, lab_l, out=self.whl)
+            K.support_lab(p, DIR_V, lab_r, out=self.wvr)
+            K.support_lab(p, DIR_H, lab_r, out=self.whr)
+            return
         K.support_lut(p, self.device, out=self.lut)
         K.asw_vSupport(p, left, self.lut, out=self.wvl)
         K.asw_hSupport(p, left, self.lut, out=self.whl)

@@ -64,9 +64,9 @@ def test_params_check_rejects(L, field, value):
     assert L.params_check(p) == L.ASW_E_INVALID
 
 
-def test_unsupported_color_space(L):
-    p = L.default_params(32, 32, color_space=L.COLOR_LAB)
-    assert L.params_check(p) == L.ASW_E_UNSUPPORTED
+def test_color_space_values(L):
+    assert L.params_check(L.default_params(32, 32, color_space=L.COLOR_LAB)) == L.ASW_OK
+    assert L.params_check(L.default_params(32, 32, color_space=7)) == L.ASW_E_INVALID
 
 
 def test_strerror(L):
