@@ -172,6 +172,10 @@ typedef struct asw_timings { /* milliseconds from HIP events, columns of main.cp
     double h2d, d2h;
 } asw_timings;
 
+/* marketing name of a HIP device (the reference names its TSV after the OpenCL
+ * device, main.cpp:164-166); writes a NUL-terminated string of at most len bytes. */
+int asw_device_name(int hip_device, char *buf, int len);
+
 /* one context = one GPU (HIP device ordinal) and one disparity shard. */
 int asw_create(const asw_params *p, int hip_device, asw_ctx **out);
 int asw_destroy(asw_ctx *ctx);

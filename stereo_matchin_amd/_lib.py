@@ -122,6 +122,7 @@ SIGNATURES = {
     "asw_wta_second": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_finalize": (I, [PP, P, P, P, P, P, P, P, P, P, P, P]),
     "asw_tune_set": (I, [I, I]),
+    "asw_device_name": (I, [I, ctypes.c_char_p, I]),
     "asw_create": (I, [PP, I, ctypes.POINTER(P)]),
     "asw_destroy": (I, [P]),
     "asw_match": (I, [P, P, P, ctypes.POINTER(AswOutputs), ctypes.POINTER(AswTimings)]),

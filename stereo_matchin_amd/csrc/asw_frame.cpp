@@ -141,6 +141,16 @@ int asw_create(const asw_params *p, int hip_device, asw_ctx **out) {
     return ASW_OK;
 }
 
+int asw_device_name(int hip_device, char *buf, int len) {
+    if (!buf || len < 1) return ASW_E_INVALID;
+    buf[0] = '\0';
+    hipDeviceProp_t prop;
+    const hipError_t e = hipGetDeviceProperties(&prop, hip_device);
+    if (e != hipSuccess) return hip_fail(e);
+    std::snprintf(buf, (size_t)len, "%s", prop.name[0] ? prop.name : prop.gcnArchName);
+    return ASW_OK;
+}
+
 int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, asw_outputs *o, asw_timings *t) {
     if (!c || !left_rgba || !right_rgba) return ASW_E_INVALID;
     HIPCHK(hipSetDevice(c->device));

@@ -1,0 +1,208 @@
+// asw_stereo — command-line host driver: the reference main.cpp's ASW flow on the
+// MI355X library, through the C-ABI of include/asw.h only.
+//
+// Mirrors stereo_matching/main.cpp:
+//   * pics.txt lists image paths, two per pair (left, right) (main.cpp:136-147);
+//     the output folder of a pair is its left path up to the first '/'
+//     (main.cpp:150-155);
+//   * images are decoded to RGBA8 (lodepng::decode in the reference,
+//     main.cpp:183-186; png_io.cpp here);
+//   * every pair runs `runs` times (main.cpp:213: 10) and the per-stage times of
+//     each run go to a TSV file named after the device (main.cpp:164-166, 181,
+//     634-708), here from HIP events (asw_timings);
+//   * outputs: <folder>/asw_consistency_pre-reff.png (the reference's file of the
+//     same name, main.cpp:625-627), asw_consistency.png (its `consistency_error`
+//     image) and asw_wta_disparity.png (its `asw_left_wta` image; the reference's
+//     asw_disparity.png is the post-refinement + median map, not produced here);
+//   * errors are printed and the driver continues with the next pair, like ErCheck
+//     (main.cpp:27-30).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "asw.h"
+#include "png_io.h"
+
+using asw_host::Image;
+
+namespace {
+
+struct Options {
+    std::string pics = "pics.txt";
+    std::string root;  // default: directory of pics
+    std::string tsv;   // default: "<device name>.tsv" in the current directory
+    int runs = 10, ndisp = 61, taps = 33, iters = 7, device = 0;
+    float gamma_c = -1.0f, gamma_g = -1.0f, tau = -1.0f;
+    bool lab = false, lr = true, native_lr = false;
+};
+
+void usage() {
+    std::fprintf(stderr,
+                 "usage: asw_stereo [--pics FILE] [--root DIR] [--runs N] [--ndisp D] [--taps T] [--iters R]\n"
+                 "                  [--gamma-c G] [--gamma-g G] [--tau TAU] [--lab] [--no-lr] [--native-lr]\n"
+                 "                  [--device I] [--tsv FILE]\n");
+}
+
+bool parse(int argc, char **argv, Options &o) {
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto next = [&](const char *what) -> const char * {
+            if (i + 1 >= argc) {
+                std::fprintf(stderr, "%s needs a value\n", what);
+                return nullptr;
+            }
+            return argv[++i];
+        };
+        const char *v = nullptr;
+        if (a == "--pics") { if (!(v = next("--pics"))) return false; o.pics = v; }
+        else if (a == "--root") { if (!(v = next("--root"))) return false; o.root = v; }
+        else if (a == "--tsv") { if (!(v = next("--tsv"))) return false; o.tsv = v; }
+        else if (a == "--runs") { if (!(v = next("--runs"))) return false; o.runs = std::atoi(v); }
+        else if (a == "--ndisp") { if (!(v = next("--ndisp"))) return false; o.ndisp = std::atoi(v); }
+        else if (a == "--taps") { if (!(v = next("--taps"))) return false; o.taps = std::atoi(v); }
+        else if (a == "--iters") { if (!(v = next("--iters"))) return false; o.iters = std::atoi(v); }
+        else if (a == "--device") { if (!(v = next("--device"))) return false; o.device = std::atoi(v); }
+        else if (a == "--gamma-c") { if (!(v = next("--gamma-c"))) return false; o.gamma_c = (float)std::atof(v); }
+        else if (a == "--gamma-g") { if (!(v = next("--gamma-g"))) return false; o.gamma_g = (float)std::atof(v); }
+        else if (a == "--tau") { if (!(v = next("--tau"))) return false; o.tau = (float)std::atof(v); }
+        else if (a == "--lab") o.lab = true;
+        else if (a == "--no-lr") o.lr = false;
+        else if (a == "--native-lr") o.native_lr = true;
+        else if (a == "-h" || a == "--help") { usage(); std::exit(0); }
+        else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return false; }
+    }
+    if (o.runs < 1) o.runs = 1;
+    return true;
+}
+
+std::string dir_of(const std::string &path) {
+    const size_t k = path.find_last_of('/');
+    return k == std::string::npos ? std::string(".") : path.substr(0, k);
+}
+
+std::string join(const std::string &a, const std::string &b) {
+    if (b.empty() || b[0] == '/') return b;
+    return a.empty() || a == "." ? b : a + "/" + b;
+}
+
+bool read_pairs(const std::string &path, std::vector<std::string> &left, std::vector<std::string> &right) {
+    FILE *fp = std::fopen(path.c_str(), "r");
+    if (!fp) return false;
+    std::vector<std::string> items;
+    char buf[4096];
+    while (std::fscanf(fp, "%4095s", buf) == 1) items.emplace_back(buf);
+    std::fclose(fp);
+    for (size_t i = 0; i + 1 < items.size(); i += 2) {
+        left.push_back(items[i]);
+        right.push_back(items[i + 1]);
+    }
+    return true;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    Options o;
+    if (!parse(argc, argv, o)) {
+        usage();
+        return 2;
+    }
+    if (o.root.empty()) o.root = dir_of(o.pics);
+    std::vector<std::string> lefts, rights;
+    if (!read_pairs(o.pics, lefts, rights)) {
+        std::fprintf(stderr, "cannot read %s\n", o.pics.c_str());
+        return 1;
+    }
+    char devname[256] = "hip-device";
+    asw_device_name(o.device, devname, (int)sizeof devname);
+    std::printf("\t- Device name: %s\n", devname);
+    const std::string tsv_path = o.tsv.empty() ? std::string(devname) + ".tsv" : o.tsv;
+    FILE *tsv = std::fopen(tsv_path.c_str(), "w");
+    if (!tsv) std::fprintf(stderr, "cannot write %s (timings go to stdout only)\n", tsv_path.c_str());
+
+    int failures = 0;
+    for (size_t k = 0; k < lefts.size(); ++k) {
+        const std::string folder = lefts[k].substr(0, lefts[k].find('/'));
+        std::printf("\n%s\n", folder.c_str());
+        Image L, R;
+        std::string e = asw_host::png_load(join(o.root, lefts[k]), L);
+        if (e.empty()) e = asw_host::png_load(join(o.root, rights[k]), R);
+        if (e.empty() && (L.width != R.width || L.height != R.height)) e = "left and right sizes differ";
+        if (!e.empty()) {
+            std::fprintf(stderr, "%s: %s\n", folder.c_str(), e.c_str());
+            ++failures;
+            continue;
+        }
+        asw_params p;
+        asw_params_default(&p);
+        p.width = (int)L.width;
+        p.height = (int)L.height;
+        p.ndisp = o.ndisp;
+        p.taps = o.taps;
+        p.iters = o.iters;
+        if (o.gamma_c > 0) p.gamma_c = o.gamma_c;
+        if (o.gamma_g > 0) p.gamma_g = o.gamma_g;
+        if (o.tau > 0) p.tad_tau = o.tau;
+        p.color_space = o.lab ? ASW_COLOR_LAB : ASW_COLOR_RGB;
+        p.lr_check = o.lr ? 1 : 0;
+        p.lr_mode = o.native_lr ? ASW_LR_NATIVE : ASW_LR_U8;
+        asw_ctx *ctx = nullptr;
+        int st = asw_create(&p, o.device, &ctx);
+        if (st != ASW_OK) {
+            std::fprintf(stderr, "%s: asw_create: %s (hip %d)\n", folder.c_str(), asw_strerror(st),
+                         asw_last_hip_error());
+            ++failures;
+            continue;
+        }
+        const size_t S = (size_t)p.width * p.height;
+        std::vector<uint8_t> disp(S * 4), lr(S * 4), lr_red(S * 4);
+        asw_outputs out;
+        std::memset(&out, 0, sizeof out);
+        out.disp_rgba = disp.data();
+        out.lr_rgba = lr.data();
+        out.lr_red_rgba = lr_red.data();
+        if (tsv) {
+            std::fprintf(tsv, "\n%s - %s\n", devname, folder.c_str());
+            std::fprintf(tsv, "id\taggr\tsupp_w\tv_aggr_mean\th_aggr_mean\ttotal aggregation\twta\tconsistency\t"
+                              "total\th2d\td2h\n");
+        }
+        for (int run = 0; run < o.runs && st == ASW_OK; ++run) {
+            asw_timings t;
+            std::memset(&t, 0, sizeof t);
+            st = asw_match(ctx, L.rgba.data(), R.rgba.data(), &out, &t);
+            if (st != ASW_OK) break;
+            std::printf("run %d: total %.3f ms (aggregation %.3f, V %.3f, H %.3f per pass)\n", run, t.total,
+                        t.aggregation_total, t.v_pass_mean, t.h_pass_mean);
+            if (tsv)
+                std::fprintf(tsv, "%d\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\n", run,
+                             t.raw_cost, t.support, t.v_pass_mean, t.h_pass_mean, t.aggregation_total, t.wta,
+                             t.consistency, t.total, t.h2d, t.d2h);
+        }
+        asw_destroy(ctx);
+        if (st != ASW_OK) {
+            std::fprintf(stderr, "%s: asw_match: %s (hip %d)\n", folder.c_str(), asw_strerror(st),
+                         asw_last_hip_error());
+            ++failures;
+            continue;
+        }
+        const std::string dir = join(o.root, folder);
+        struct {
+            const char *name;
+            const std::vector<uint8_t> *img;
+        } outs[] = {{"asw_wta_disparity.png", &disp},
+                    {"asw_consistency.png", &lr},
+                    {"asw_consistency_pre-reff.png", &lr_red}};
+        for (const auto &w : outs) {
+            if (!p.lr_check && w.img != &disp) continue;
+            e = asw_host::png_save(dir + "/" + w.name, w.img->data(), L.width, L.height, 4);
+            if (!e.empty()) {
+                std::fprintf(stderr, "%s: %s\n", folder.c_str(), e.c_str());
+                ++failures;
+            }
+        }
+    }
+    if (tsv) std::fclose(tsv);
+    return failures ? 1 : 0;
+}
