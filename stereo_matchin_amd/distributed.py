@@ -31,6 +31,22 @@ from ._lib import AswParams
 from .pipeline import MatchResult, StereoMatcher
 
 
+def plan_groups(ndisp: int, world: int, min_planes: int = 64) -> int:
+    """Ranks per d-sharded frame ("group size") for `world` ranks.
+
+    The pass kernels work on 64-plane blocks, so a shard narrower than 64 planes
+    pads its work up to 64 and gains nothing from the split.  The group size is
+    the largest divisor g of `world` with ndisp/g >= min_planes (1 if none):
+    world/g groups then each match their own frame, concurrently (e.g. D=256 on 8
+    GPUs: 2 frames, each d-sharded 4 ways; on 2 or 4 GPUs one frame).
+    """
+    best = 1
+    for g in range(1, world + 1):
+        if world % g == 0 and ndisp / g >= min_planes:
+            best = g
+    return best
+
+
 def shard_range(ndisp: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous balanced split of [0, ndisp) into `world` non-empty shards."""
     if world > ndisp:

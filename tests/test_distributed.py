@@ -124,6 +124,54 @@ def _worker(rank, world, port, D, H, W, seed, out_path):
         dist.destroy_process_group()
 
 
+def _group_worker(rank, world, G, port, D, H, W, out_dir):
+    """bench.py's layout: world/G frame groups, each d-sharded over its G ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        groups, gid, grank = world // G, rank // G, rank % G
+        subs = [dist.new_group(list(range(g * G, (g + 1) * G))) for g in range(groups)]
+        pg = subs[gid]
+        C = _volume(D, H, W, 777 + gid)  # one frame per group
+        b, e = shard_range(D, grank, G)
+        local = torch.from_numpy(np.ascontiguousarray(C[b:e].transpose(1, 2, 0)))
+
+        def reduce_min(t):
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=pg)
+            return t
+
+        d_ref, conf_ref, d_tar, conf_tar = sharded_wta(CpuShardOps(b, e, D), local, reduce_min)
+        stat = torch.tensor([float(rank)])
+        dist.all_reduce(stat, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks on the world group
+        assert stat.item() == world - 1
+        if grank == 0:
+            np.savez(os.path.join(out_dir, f"g{gid}.npz"), d_ref=d_ref, d_tar=d_tar, conf_ref=conf_ref,
+                     conf_tar=conf_tar)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_frame_groups_gloo(oracle, tmp_path):
+    from stereo_matchin_amd.distributed import plan_groups
+    world, D, H, W = 4, 16, 4, 18
+    G = plan_groups(D, world, min_planes=8)
+    assert G == 2
+    mp.start_processes(_group_worker, args=(world, G, _free_port(), D, H, W, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    for gid in range(world // G):
+        got = np.load(tmp_path / f"g{gid}.npz")
+        dr, cr, dt, ct = oracle.wta(_volume(D, H, W, 777 + gid))
+        assert np.array_equal(got["d_ref"], dr) and np.array_equal(got["d_tar"], dt)
+        np.testing.assert_array_equal(got["conf_ref"], cr)
+        np.testing.assert_array_equal(got["conf_tar"], ct)
+
+
+def test_plan_groups():
+    from stereo_matchin_amd.distributed import plan_groups
+    assert [plan_groups(256, n) for n in (1, 2, 4, 8)] == [1, 2, 4, 4]
+    assert plan_groups(512, 8) == 8 and plan_groups(61, 2) == 1 and plan_groups(128, 8) == 2
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
