@@ -79,25 +79,34 @@ __global__ void k_support_lut(float *lut, int rows, float gamma_c, float gamma_g
 // asw_Aggr (K/asw_aggr.cl:3-23): per-disparity absolute-difference cost.
 // One thread per (pixel, local plane); d fastest => coalesced stores.
 // ---------------------------------------------------------------------------
-__global__ void k_raw_cost(const uchar4 *__restrict__ L, const uchar4 *__restrict__ R, float *__restrict__ cost,
-                           int W, int H, int Dp, int nloc, int d_begin, float tau) {
-    const long long n = (long long)W * H * Dp;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const int k = (int)(idx % Dp);
-        const long long p = idx / Dp;
-        float v = 0.0f;
-        if (k < nloc) {
-            const int x = (int)(p % W), y = (int)(p / W);
-            const int d = d_begin + k;
-            const int xr = x - d < 0 ? 0 : x - d;
-            const uchar4 l = L[p];
-            const uchar4 r = R[(long long)y * W + xr];
-            float s = fabsf((float)l.x - (float)r.x) + fabsf((float)l.y - (float)r.y);
-            s = s + fabsf((float)l.z - (float)r.z);
-            v = fminf(s, tau);
+__global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, const uchar4 *__restrict__ R,
+                                                   float *__restrict__ cost, int W, int Dp, int nloc, int d_begin,
+                                                   float tau, int px_per_wave) {
+    // block = 4 waves on row blockIdx.y; a wave writes whole pixels, 4 planes per
+    // lane per store (float4): 1 KB per wave-instruction, no 64-bit index math.
+    using f4 = float __attribute__((ext_vector_type(4)));
+    const int y = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uchar4 *Lrow = L + (long long)y * W, *Rrow = R + (long long)y * W;
+    const int nq = Dp >> 2;
+    const int x0 = (blockIdx.x * 4 + wave) * px_per_wave;
+    const int x1 = min(x0 + px_per_wave, W);
+    for (int x = x0; x < x1; ++x) {
+        const uchar4 l = Lrow[x];
+        f4 *out = reinterpret_cast<f4 *>(cost + ((long long)y * W + x) * Dp);
+        for (int q = lane; q < nq; q += 64) {
+            f4 v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = 4 * q + j;
+                const int d = d_begin + k;
+                const uchar4 r = Rrow[x - d < 0 ? 0 : x - d];
+                float sv = fabsf((float)l.x - (float)r.x) + fabsf((float)l.y - (float)r.y);
+                sv = sv + fabsf((float)l.z - (float)r.z);
+                v[j] = k < nloc ? fminf(sv, tau) : 0.0f;
+            }
+            out[q] = v;
         }
-        cost[idx] = v;
     }
 }
 
@@ -105,32 +114,31 @@ __global__ void k_raw_cost(const uchar4 *__restrict__ L, const uchar4 *__restric
 // asw_vSupport / asw_hSupport (K/asw_vsupport.cl:3-27, K/asw_hsupport.cl:3-28).
 // w[y][x][i] = LUT[|delta|][SAD(p,q)], q the i-th tap of p's 1-D window.
 // ---------------------------------------------------------------------------
-__global__ void k_support(const uchar4 *__restrict__ img, const float *__restrict__ lut, float *__restrict__ w,
-                          int W, int H, int T, int Tp, int dir) {
-    const long long n = (long long)W * H * Tp;
+// Row y = blockIdx.y; thread t of the row covers (x, i) = (t / Tp, t % Tp), so
+// consecutive threads store consecutive floats; 32-bit index math only.
+__global__ __launch_bounds__(256) void k_support(const uchar4 *__restrict__ img, const float *__restrict__ lut,
+                                                 float *__restrict__ w, int W, int H, int T, int Tp, int dir) {
+    const int y = blockIdx.y;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= W * Tp) return;
+    const int x = t / Tp, i = t - x * Tp;
     const int R = T / 2;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const int i = (int)(idx % Tp);
-        const long long p = idx / Tp;
-        float v = 0.0f;
-        if (i < T) {
-            const int x = (int)(p % W), y = (int)(p / W);
-            int qx = x, qy = y, dist;
-            if (dir == ASW_DIR_V) {
-                qy = clampi(y + i - R, 0, H - 1);
-                dist = y > qy ? y - qy : qy - y;
-            } else {
-                qx = clampi(x + i - R, 0, W - 1);
-                dist = x > qx ? x - qx : qx - x;
-            }
-            const uchar4 a = img[p];
-            const uchar4 b = img[(long long)qy * W + qx];
-            const int sad = abs((int)a.x - (int)b.x) + abs((int)a.y - (int)b.y) + abs((int)a.z - (int)b.z);
-            v = lut[dist * kLutWidth + sad];
+    float v = 0.0f;
+    if (i < T) {
+        int qx = x, qy = y, dist;
+        if (dir == ASW_DIR_V) {
+            qy = clampi(y + i - R, 0, H - 1);
+            dist = y > qy ? y - qy : qy - y;
+        } else {
+            qx = clampi(x + i - R, 0, W - 1);
+            dist = x > qx ? x - qx : qx - x;
         }
-        w[idx] = v;
+        const uchar4 a = img[y * W + x];
+        const uchar4 b = img[qy * W + qx];
+        const int sad = abs((int)a.x - (int)b.x) + abs((int)a.y - (int)b.y) + abs((int)a.z - (int)b.z);
+        v = lut[dist * kLutWidth + sad];
     }
+    w[(long long)y * W * Tp + t] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -169,37 +177,34 @@ __global__ void k_lab(const uchar4 *__restrict__ img, float4 *__restrict__ lab, 
 // K/asw_vsupport.cl:19-25 with the RGB SAD replaced by the Euclidean distance
 // dc = sqrt((dL^2 + da^2) + db^2) (float sums; the double sqrt rounded to float
 // is the correctly rounded float sqrt), exp as exp_d.
-__global__ void k_support_lab(const float4 *__restrict__ lab, float *__restrict__ w, int W, int H, int T, int Tp,
-                              int dir, float gamma_c, float gamma_g) {
-    const long long n = (long long)W * H * Tp;
+__global__ __launch_bounds__(256) void k_support_lab(const float4 *__restrict__ lab, float *__restrict__ w, int W,
+                                                     int H, int T, int Tp, int dir, float gamma_c, float gamma_g) {
+    const int y = blockIdx.y;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= W * Tp) return;
+    const int x = t / Tp, i = t - x * Tp;
     const int R = T / 2;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const int i = (int)(idx % Tp);
-        const long long p = idx / Tp;
-        float v = 0.0f;
-        if (i < T) {
-            const int x = (int)(p % W), y = (int)(p / W);
-            int qx = x, qy = y, dist;
-            if (dir == ASW_DIR_V) {
-                qy = clampi(y + i - R, 0, H - 1);
-                dist = y > qy ? y - qy : qy - y;
-            } else {
-                qx = clampi(x + i - R, 0, W - 1);
-                dist = x > qx ? x - qx : qx - x;
-            }
-            const float4 a = lab[p];
-            const float4 b = lab[(long long)qy * W + qx];
-            const float dL = a.x - b.x, da = a.y - b.y, db = a.z - b.z;
-            float s2 = dL * dL + da * da;
-            s2 = s2 + db * db;
-            const float dc = (float)sqrt((double)s2);
-            const float c_diff = (-dc) / gamma_c;
-            const float g_dist = (float)dist / gamma_g;
-            v = (float)exp_d((double)(c_diff - g_dist));
+    float v = 0.0f;
+    if (i < T) {
+        int qx = x, qy = y, dist;
+        if (dir == ASW_DIR_V) {
+            qy = clampi(y + i - R, 0, H - 1);
+            dist = y > qy ? y - qy : qy - y;
+        } else {
+            qx = clampi(x + i - R, 0, W - 1);
+            dist = x > qx ? x - qx : qx - x;
         }
-        w[idx] = v;
+        const float4 a = lab[y * W + x];
+        const float4 b = lab[qy * W + qx];
+        const float dL = a.x - b.x, da = a.y - b.y, db = a.z - b.z;
+        float s2 = dL * dL + da * da;
+        s2 = s2 + db * db;
+        const float dc = (float)sqrt((double)s2);
+        const float c_diff = (-dc) / gamma_c;
+        const float g_dist = (float)dist / gamma_g;
+        v = (float)exp_d((double)(c_diff - g_dist));
     }
+    w[(long long)y * W * Tp + t] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -240,6 +245,15 @@ __device__ __forceinline__ void top2_wave_reduce(Top2 &s) {
 
 constexpr float kInit = 100000.0f;  // K/asw_wta.cl:25-26
 
+// Pixel of this wave in the WTA kernels: blocks of 4 waves = 4 consecutive
+// pixels; XCD j (blockIdx % 8) walks its own contiguous range of pixels in
+// order, so the row a target scan re-reads (the diagonal of the volume) was just
+// streamed through that XCD's L2 by the same XCD's main scans.
+__device__ __forceinline__ long long wta_pixel(int blocks_per_xcd) {
+    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
+    return ((long long)xcd * blocks_per_xcd + m) * 4 + (threadIdx.x >> 6);
+}
+
 // Target (right-view) scan of asw_WTA (K/asw_wta.cl:50-67): for i < md,
 // xq = max(0,x-i), b = md + xq - x (the bresenham() line of :3-9 always has
 // slope 1), candidate C[b][y][xq].  Only b in [b_lo, b_hi) (the local shard) is
@@ -261,12 +275,12 @@ __device__ __forceinline__ Top2 target_scan(const float *__restrict__ cost, int 
 
 // asw_WTA (K/asw_wta.cl:12-82) for a context owning all D planes.
 // One wave per pixel: lanes scan d = lane, lane+64, ... then a shuffle reduction.
-__global__ __launch_bounds__(256) void k_wta(const float *__restrict__ cost, int W, int H, int Dp, int D,
+__global__ __launch_bounds__(256) void k_wta(const float *__restrict__ cost, int W, int H, int Dp, int D, int bpx,
                                              int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
                                              int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
                                              uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar) {
     const int lane = threadIdx.x & 63;
-    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long p = wta_pixel(bpx);
     if (p >= (long long)W * H) return;
     const int x = (int)(p % W), y = (int)(p / W);
     const float *cp = cost + p * Dp;
@@ -292,11 +306,11 @@ __device__ __forceinline__ long long make_key(float v, int idx) {
 constexpr long long kNoKey = 0x7fffffffffffffffLL;
 
 // d-sharded left WTA, local half: planes [d_begin, d_end) of the shard.
-__global__ __launch_bounds__(256) void k_wta_local(const float *__restrict__ cost, int W, int H, int Dp,
+__global__ __launch_bounds__(256) void k_wta_local(const float *__restrict__ cost, int W, int H, int Dp, int bpx,
                                                    int d_begin, int nloc, long long *__restrict__ key,
                                                    float *__restrict__ m1, float *__restrict__ m2) {
     const int lane = threadIdx.x & 63;
-    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long p = wta_pixel(bpx);
     if (p >= (long long)W * H) return;
     const float *cp = cost + p * Dp;
     Top2 s{kInit, kInit, INT_MAX};
@@ -309,13 +323,13 @@ __global__ __launch_bounds__(256) void k_wta_local(const float *__restrict__ cos
     }
 }
 
-__global__ __launch_bounds__(256) void k_wta_target_local(const float *__restrict__ cost, int W, int H, int Dp,
+__global__ __launch_bounds__(256) void k_wta_target_local(const float *__restrict__ cost, int W, int H, int Dp, int bpx,
                                                           int d_begin, int d_end,
                                                           const long long *__restrict__ key_ref,
                                                           long long *__restrict__ tkey, float *__restrict__ t1,
                                                           float *__restrict__ t2) {
     const int lane = threadIdx.x & 63;
-    const long long p = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long p = wta_pixel(bpx);
     if (p >= (long long)W * H) return;
     const int x = (int)(p % W), y = (int)(p / W);
     const long long kr = key_ref[p];
@@ -405,10 +419,6 @@ inline int finish_launch() {
     return ASW_OK;
 }
 
-inline int grid_for(long long n, int block) {
-    long long g = (n + block - 1) / block;
-    return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
-}
 
 }  // namespace
 }  // namespace asw
@@ -494,10 +504,11 @@ size_t asw_lut_bytes(const asw_params *p) { return (size_t)(p->taps / 2 + 1) * k
 int asw_raw_cost(const asw_params *p, const uint8_t *left, const uint8_t *right, float *cost, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!left || !right || !cost) return ASW_E_INVALID;
-    const long long n = (long long)p->width * p->height * asw_disp_pitch(p);
-    hipLaunchKernelGGL(k_raw_cost, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const uchar4 *>(left), reinterpret_cast<const uchar4 *>(right), cost,
-                       p->width, p->height, asw_disp_pitch(p), d_end_of(p) - p->d_begin, p->d_begin, p->tad_tau);
+    const int ppw = 8;  // pixels per wave
+    const dim3 grid((unsigned)((p->width + 4 * ppw - 1) / (4 * ppw)), (unsigned)p->height);
+    hipLaunchKernelGGL(k_raw_cost, grid, dim3(256), 0, (hipStream_t)stream, reinterpret_cast<const uchar4 *>(left),
+                       reinterpret_cast<const uchar4 *>(right), cost, p->width, asw_disp_pitch(p),
+                       d_end_of(p) - p->d_begin, p->d_begin, p->tad_tau, ppw);
     return finish_launch();
 }
 
@@ -516,8 +527,8 @@ int asw_support(const asw_params *p, int dir, const uint8_t *img, const float *l
     if (!img || !lut || !w || (dir != ASW_DIR_V && dir != ASW_DIR_H)) return ASW_E_INVALID;
     if (p->color_space != ASW_COLOR_RGB) return ASW_E_INVALID;  // LAB contexts: asw_support_lab
     const int Tp = asw_tap_pitch(p);
-    const long long n = (long long)p->width * p->height * Tp;
-    hipLaunchKernelGGL(k_support, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+    const dim3 grid((unsigned)((p->width * Tp + 255) / 256), (unsigned)p->height);
+    hipLaunchKernelGGL(k_support, grid, dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const uchar4 *>(img), lut, w, p->width, p->height, p->taps, Tp, dir);
     return finish_launch();
 }
@@ -536,8 +547,8 @@ int asw_support_lab(const asw_params *p, int dir, const float *lab, float *w, vo
     if (!lab || !w || (dir != ASW_DIR_V && dir != ASW_DIR_H)) return ASW_E_INVALID;
     if (p->color_space != ASW_COLOR_LAB) return ASW_E_INVALID;
     const int Tp = asw_tap_pitch(p);
-    const long long n = (long long)p->width * p->height * Tp;
-    hipLaunchKernelGGL(k_support_lab, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+    const dim3 grid((unsigned)((p->width * Tp + 255) / 256), (unsigned)p->height);
+    hipLaunchKernelGGL(k_support_lab, grid, dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const float4 *>(lab), w, p->width, p->height, p->taps, Tp, dir, p->gamma_c,
                        p->gamma_g);
     return finish_launch();
@@ -569,8 +580,9 @@ int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_
     if (p->d_begin != 0 || d_end_of(p) != p->ndisp) return ASW_E_INVALID;  // sharded: use asw_wta_local & co.
     if (!cost || !d_ref || !conf_ref || !d_tar || !conf_tar) return ASW_E_INVALID;
     const long long n = (long long)p->width * p->height;
-    hipLaunchKernelGGL(k_wta, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, cost, p->width,
-                       p->height, asw_disp_pitch(p), p->ndisp, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar);
+    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
+    hipLaunchKernelGGL(k_wta, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost, p->width,
+                       p->height, asw_disp_pitch(p), p->ndisp, bpx, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar);
     return finish_launch();
 }
 
@@ -578,8 +590,9 @@ int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m
     ASW_CHECK_PARAMS(p);
     if (!cost || !key || !m1 || !m2) return ASW_E_INVALID;
     const long long n = (long long)p->width * p->height;
-    hipLaunchKernelGGL(k_wta_local, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, cost,
-                       p->width, p->height, asw_disp_pitch(p), p->d_begin, d_end_of(p) - p->d_begin,
+    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
+    hipLaunchKernelGGL(k_wta_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
+                       p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p) - p->d_begin,
                        reinterpret_cast<long long *>(key), m1, m2);
     return finish_launch();
 }
@@ -589,8 +602,9 @@ int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *
     ASW_CHECK_PARAMS(p);
     if (!cost || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
     const long long n = (long long)p->width * p->height;
-    hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, cost,
-                       p->width, p->height, asw_disp_pitch(p), p->d_begin, d_end_of(p),
+    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
+    hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
+                       p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p),
                        reinterpret_cast<const long long *>(key_ref), reinterpret_cast<long long *>(tkey), t1, t2);
     return finish_launch();
 }

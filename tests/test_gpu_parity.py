@@ -131,6 +131,34 @@ def test_single_pass_sharded_planes(gpu, oracle, direction):
     assert np.array_equal(got, want)
 
 
+# every compiled pass variant (asw_tune_set): block shapes, 8-wave V, and the
+# diagonal-pair H kernel (Dp % 128 == 0), on shapes that hit segment / row edges
+@pytest.mark.parametrize("variant", [0, 2, 4, 8, 16])
+@pytest.mark.parametrize("H,W,D,d0,d1", [(9, 331, 256, 0, 256), (6, 47, 128, 0, 128), (5, 161, 300, 40, 168),
+                                          (4, 400, 256, 128, 256)])
+def test_pass_variants_bit_exact(gpu, oracle, variant, H, W, D, d0, d1):
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    T = 35
+    Lh, Rh = _rand_pair(variant * 31 + W, H, W, shift=5)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
+    Dp = K.cost_shape(p)[2]
+    rng = np.random.default_rng(W + variant)
+    cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+    old = _lib.lib().asw_tune_set(1, variant)
+    try:
+        for direction in (0, 1):
+            sl, sr = oracle.support(Lh, T, direction), oracle.support(Rh, T, direction)
+            want = oracle.aggregate_pass(sl, sr, cin, T, direction, d0=d0, d1=d1, plane_base=d0)
+            f = K.asw_vSupport if direction == 0 else K.asw_hSupport
+            g = K.asw_vCostAggregation if direction == 0 else K.asw_hCostAggregation
+            out = g(p, f(p, _t(Lh, gpu)), f(p, _t(Rh, gpu)), _t(pixel_major(cin, Dp), gpu))
+            got = plane_major(_np(out), d1 - d0)
+            assert np.array_equal(got, want), (variant, direction, np.argwhere(got != want)[:5])
+    finally:
+        _lib.lib().asw_tune_set(1, old)
+
+
 def test_wta_and_consistency_on_oracle_volume(gpu, oracle):
     import stereo_matchin_amd.kernels as K
     Lh, Rh, _ = load_scene("tsukuba")
