@@ -18,7 +18,9 @@ import re
 import torch  # noqa: F401  (must precede loading libasw_hip.so, see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libasw_hip.so")
+# ASW_LIB overrides the library path (kernel experiments: tools/ builds variants
+# of the same sources into another file); the default is the in-tree build.
+LIB_PATH = os.environ.get("ASW_LIB") or os.path.join(_HERE, "libasw_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "asw.h")
 
 ASW_OK = 0

@@ -24,6 +24,11 @@ __device__ __forceinline__ void taps_v(float &num, float &den, const f4 (&wl)[M1
         den = den + ww;
     }
 }
+template <int U, int S, int B, int E, int N, int M>
+__device__ __forceinline__ void taps_nd(float &num, const float (&wl)[N], const f4 (&wr)[M], const float (&win)[U]) {
+#pragma unroll
+    for (int i = B; i < E; ++i) num = __builtin_fmaf(wl[i - B] * wr[(i - B) / 4][(i - B) % 4], win[(S + i) % U], num);
+}
 template <int T, int QB, int QE, int M>
 __device__ __forceinline__ void load_wl_v(f4 (&dst)[M], const float *px, int z) {
 #pragma unroll
@@ -78,6 +83,12 @@ __global__ __launch_bounds__(NW * 64) void k_hexp(const float *__restrict__ wl, 
     using HV = Halves<T>;
     float win[U];
     float warm[PW];
+    float dring[8];  // EXP 256: cached denominators, loaded 6 steps ahead
+    const float *dbase = cin + (long long)((y + 1) % H) * W * Dp + k;  // stand-in den volume (timing only)
+    if constexpr ((EXP & 256) != 0) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) dring[j] = dbase[(long long)min(xw0 + j, W - 1) * Dp];
+    }
     float sink = 0.0f;
     float wla[HV::NA], wlb[HV::NB];
     f4 wra[HV::MA], wrb[HV::MB];
@@ -121,6 +132,7 @@ __global__ __launch_bounds__(NW * 64) void k_hexp(const float *__restrict__ wl, 
         __builtin_amdgcn_sched_barrier(0);
         float num = 1e-5f, den = 1e-5f;
         if constexpr ((EXP & 16) != 0) taps_v<U, s, 0, HV::TA>(num, den, wlva, wra, win);
+        else if constexpr ((EXP & 256) != 0) taps_nd<U, s, 0, HV::TA>(num, wla, wra, win);
         else taps<U, s, 0, HV::TA>(num, den, wla, wra, win);
         __builtin_amdgcn_sched_barrier(0);
         wait_lgkm0();  // half B's weights
@@ -135,7 +147,12 @@ __global__ __launch_bounds__(NW * 64) void k_hexp(const float *__restrict__ wl, 
         if constexpr ((EXP & 4) != 0) asm volatile("" ::"s"(qwl), "v"(qwr));
         __builtin_amdgcn_sched_barrier(0);
         if constexpr ((EXP & 16) != 0) taps_v<U, s, HV::TA, T>(num, den, wlvb, wrb, win);
+        else if constexpr ((EXP & 256) != 0) taps_nd<U, s, HV::TA, T>(num, wlb, wrb, win);
         else if constexpr (HV::TB > 0) taps<U, s, HV::TA, T>(num, den, wlb, wrb, win);
+        if constexpr ((EXP & 256) != 0) {
+            den = dring[s % 8] + 1.0f;  // + 1: a stand-in volume of costs is a valid positive divisor
+            dring[(s + 6) % 8] = dbase[(long long)min(x + 6, W - 1) * Dp];
+        }
         obase[(long long)x * Dp] = div_pos(num, den);
         win[(s + U - 1) % U] = cbase[(long long)clampi(x + R + P, 0, W - 1) * Dp];
         sink += warm[s % PW];
@@ -195,16 +212,17 @@ int main() {
     CK(hipMemcpy(wr, h.data(), ns * 4, hipMemcpyHostToDevice));
     CK(hipMemset(cin, 0x3f, nc * 4));
     const double bytes = 8.0 * 256 * W * H + 8.0 * 35 * W * H;
-    const int exps[] = {0, 3, 32, 64, 96, 1};
-    const char *names[] = {"full", "no weight loads", "SMEM from one constant pixel (scalar-cache hits)",
-                           "LDS reads of one constant entry", "both constant", "no SMEM"};
+    const int exps[] = {0, 256, 3, 32, 64, 1};
+    const char *names[] = {"full", "cached denominators (den read per voxel, no den adds)", "no weight loads",
+                           "SMEM from one constant pixel (scalar-cache hits)", "LDS reads of one constant entry",
+                           "no SMEM"};
     float ms[6];
     for (int rep = 0; rep < 2; ++rep) {
         ms[0] = run<0>(wl, wr, cin, cout, W, H, Dp, 10);
-        ms[1] = run<3>(wl, wr, cin, cout, W, H, Dp, 10);
-        ms[2] = run<32>(wl, wr, cin, cout, W, H, Dp, 10);
-        ms[3] = run<64>(wl, wr, cin, cout, W, H, Dp, 10);
-        ms[4] = run<96>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[1] = run<256>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[2] = run<3>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[3] = run<32>(wl, wr, cin, cout, W, H, Dp, 10);
+        ms[4] = run<64>(wl, wr, cin, cout, W, H, Dp, 10);
         ms[5] = run<1>(wl, wr, cin, cout, W, H, Dp, 10);
     }
     CK(hipGetLastError());
