@@ -396,3 +396,187 @@ int oracle_match(const uint8_t *L, const uint8_t *R, int W, int H, int D, int T,
     return oracle_match_ex(L, R, W, H, D, T, iters, gamma_c, gamma_g, fma_mode, 0, 765.0f, d_ref, conf_ref, d_tar,
                            conf_tar, out_rgba, out_red_rgba, cost_out);
 }
+
+/* ===================== refinement loop =====================
+ * main.cpp:540-623 — k iterations of
+ *   asw_ref_v (K/asw_refinement_v.cl:13-51) on (L, est_left, conf_ref) and (R, est_right, conf_tar),
+ *   asw_ref_h (K/asw_refinement_h.cl:16-53) on their outputs,
+ *   asw_WTA_REF (K/asw_wta_ref.cl:2-68) over the final aggregated volume,
+ *   Constistency (K/consist.cl) on the new codes,
+ * then the 3x3 Median (K/median.cl:58-88) of the last consistency image.
+ * Refinement weight: exp((-SAD)/10.94 - dist/118.78) (K/asw_refinement_v.cl:1-9).
+ * est images are read back as D = (code/255)*60 (general D: *(D-1)).
+ * Reproduced as written, including asw_WTA_REF storing the TARGET confidence into
+ * confidence_reference (its second write, K/asw_wta_ref.cl:64-66) and never
+ * writing confidence_target (only Constistency zeroes it), and the target
+ * penalty using |ref_target - i| with i the scan index (K/asw_wta_ref.cl:45).
+ *
+ * Contraction policy `pol` (the vendor compiler's choice is not in the source;
+ * tests/test_oracle_golden.py picks the one the device PNGs agree with):
+ *   bit 0: V num = fma(w*F, D, num)        else num + (w*F)*D
+ *   bit 1: V den = fma(w, F, den)          else den + w*F
+ *   bit 2: H num = fma((w*F)*r, n, num)    else num + ((w*F)*r)*n
+ *   bit 3: H den = fma(w*F, n, den)        else den + (w*F)*n
+ *   bit 4: penalty = fma(0.085*n, |r-i|, c) else (0.085*n)*|r-i| + c          */
+#define REF_GC 10.94f
+#define REF_GG 118.78f
+
+static float ref_weight(const uint8_t *p, const uint8_t *q, int dist) {
+    const int sad = abs((int)p[0] - q[0]) + abs((int)p[1] - q[1]) + abs((int)p[2] - q[2]);
+    return oracle_support_weight(sad, dist, REF_GC, REF_GG);
+}
+
+/* out[0..S) = num/den, out[S..2S) = den */
+static void ref_v(const uint8_t *img, const uint8_t *est, const float *conf, int W, int H, int D, int Tr, int pol,
+                  float *out) {
+    const long S = (long)W * H;
+    const int Rr = Tr / 2;
+    const float scale = (float)(D - 1);
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const uint8_t *p = img + 4 * ((long)y * W + x);
+            float num = 0.00001f, den = 0.00001f;
+            for (int i = 0; i < Tr; ++i) {
+                const int qy = clampi(y + i - Rr, 0, H - 1);
+                const long q = (long)qy * W + x;
+                const float w = ref_weight(p, img + 4 * q, abs(y - qy));
+                const float Dv = ((float)est[q] / 255.0f) * scale;
+                const float F = conf[q];
+                const float t = w * F;
+                num = (pol & 1) ? fmaf(t, Dv, num) : num + t * Dv;
+                den = (pol & 2) ? fmaf(w, F, den) : den + t;
+            }
+            out[(long)y * W + x] = num / den;
+            out[S + (long)y * W + x] = den;
+        }
+}
+
+static void ref_h(const uint8_t *img, const float *conf, const float *in, int W, int H, int Tr, int pol, float *out) {
+    const long S = (long)W * H;
+    const int Rr = Tr / 2;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const uint8_t *p = img + 4 * ((long)y * W + x);
+            float num = 0.00001f, den = 0.00001f;
+            for (int i = 0; i < Tr; ++i) {
+                const int qx = clampi(x + i - Rr, 0, W - 1);
+                const long q = (long)y * W + qx;
+                const float w = ref_weight(p, img + 4 * q, abs(x - qx));
+                const float F = conf[q];
+                const float r = in[q], n = in[S + q];
+                const float t = w * F;
+                const float tr = t * r;
+                num = (pol & 4) ? fmaf(tr, n, num) : num + tr * n;
+                den = (pol & 8) ? fmaf(t, n, den) : den + t * n;
+            }
+            out[(long)y * W + x] = num / den;
+            out[S + (long)y * W + x] = den;
+        }
+}
+
+static inline float penalty(float n, float r, int i, float c, int pol) {
+    const float a = 0.085f * n;
+    const float b = fabsf(r - (float)i);
+    return (pol & 16) ? fmaf(a, b, c) : a * b + c;
+}
+
+/* asw_WTA_REF: codes of min_d / min_d_r; conf_ref <- the target confidence */
+static void wta_ref(const float *C, const float *ref, const float *ref_t, int W, int H, int D, int pol,
+                    int32_t *d_ref, int32_t *d_tar, float *conf_ref) {
+    const long S = (long)W * H;
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const long p = (long)y * W + x;
+            float cur = 100000.0f, last = 100000.0f;
+            int md = 0;
+            for (int i = 0; i < D; ++i) {
+                const float pen = penalty(ref[S + p], ref[p], i, C[(long)i * S + p], pol);
+                last = pen < last ? pen : last;
+                md = pen < cur ? i : md;
+                last = pen < cur ? cur : last;
+                cur = pen < cur ? pen : cur;
+            }
+            int mdr = md;
+            float cur_t = 100000.0f, last_t = 100000.0f;
+            for (int i = 0; i < md; ++i) {
+                const int xq = x - i < 0 ? 0 : x - i;
+                const int b = md + xq - x;
+                const float pen = penalty(ref_t[S + p], ref_t[p], i, C[(long)b * S + (long)y * W + xq], pol);
+                last_t = pen < last_t ? pen : last_t;
+                mdr = pen < cur_t ? b : mdr;
+                last_t = pen < cur_t ? cur_t : last_t;
+                cur_t = pen < cur_t ? pen : cur_t;
+            }
+            d_ref[p] = md;
+            d_tar[p] = mdr;
+            conf_ref[p] = (last_t - cur_t) / last_t;  /* the second (overwriting) write of K/asw_wta_ref.cl */
+        }
+}
+
+/* 3x3 median of a u8 code image with clamped borders (K/median.cl: the
+ * min/max network yields the exact median of the 9 samples per channel). */
+static void median3(const uint8_t *in, int W, int H, uint8_t *out) {
+#pragma omp parallel for schedule(static)
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            int hist[9], n = 0;
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) hist[n++] = in[(long)clampi(y + dy, 0, H - 1) * W + clampi(x + dx, 0, W - 1)];
+            for (int i = 1; i < 9; ++i)
+                for (int j = i; j > 0 && hist[j - 1] > hist[j]; --j) {
+                    const int t = hist[j];
+                    hist[j] = hist[j - 1];
+                    hist[j - 1] = t;
+                }
+            out[(long)y * W + x] = (uint8_t)hist[4];
+        }
+}
+
+/* The whole loop.  Inputs: final aggregated volume C [D][H][W], the codes of the
+ * pre-refinement consistency image (est_left = cons ? code_ref : code_tar) and of
+ * the initial target map (est_right = code_tar), conf_ref / conf_tar after that
+ * consistency check (modified in place).  Outputs (any may be NULL):
+ * post_red_rgba (asw_consistency_post-reff.png), final_rgba (asw_disparity.png),
+ * d_ref / d_tar of the last WTA_REF. */
+int oracle_refine(const uint8_t *L, const uint8_t *R, int W, int H, int D, int k, int Tr, int pol, const float *C,
+                  const uint8_t *est_left_in, const uint8_t *est_right_in, float *conf_ref, float *conf_tar,
+                  uint8_t *post_red_rgba, uint8_t *final_rgba, int32_t *d_ref_out, int32_t *d_tar_out) {
+    const long S = (long)W * H;
+    float *vl = (float *)malloc(sizeof(float) * 2 * S), *vr = (float *)malloc(sizeof(float) * 2 * S);
+    float *hl = (float *)malloc(sizeof(float) * 2 * S), *hr = (float *)malloc(sizeof(float) * 2 * S);
+    uint8_t *el = (uint8_t *)malloc(S), *er = (uint8_t *)malloc(S), *kl = (uint8_t *)malloc(S);
+    uint8_t *o1 = (uint8_t *)malloc(4 * S), *o2 = (uint8_t *)malloc(4 * S), *fin = (uint8_t *)malloc(S);
+    int32_t *dr = (int32_t *)malloc(sizeof(int32_t) * S), *dt = (int32_t *)malloc(sizeof(int32_t) * S);
+    if (!vl || !vr || !hl || !hr || !el || !er || !kl || !o1 || !o2 || !fin || !dr || !dt) return -1;
+    memcpy(el, est_left_in, S);
+    memcpy(er, est_right_in, S);
+    memset(o2, 0, 4 * S);
+    for (int it = 0; it < k; ++it) {
+        ref_v(L, el, conf_ref, W, H, D, Tr, pol, vl);
+        ref_v(R, er, conf_tar, W, H, D, Tr, pol, vr);
+        ref_h(L, conf_ref, vl, W, H, Tr, pol, hl);
+        ref_h(R, conf_tar, vr, W, H, Tr, pol, hr);
+        wta_ref(C, hl, hr, W, H, D, pol, dr, dt, conf_ref);
+        for (long p = 0; p < S; ++p) {
+            kl[p] = (uint8_t)oracle_code_u8(dr[p], D);
+            er[p] = (uint8_t)oracle_code_u8(dt[p], D);
+        }
+        oracle_consistency(kl, er, conf_ref, conf_tar, W, H, D, o1, o2);
+        for (long p = 0; p < S; ++p) el[p] = o1[4 * p];
+    }
+    median3(el, W, H, fin);
+    if (post_red_rgba) memcpy(post_red_rgba, o2, 4 * S);
+    if (final_rgba)
+        for (long p = 0; p < S; ++p) {
+            final_rgba[4 * p] = final_rgba[4 * p + 1] = final_rgba[4 * p + 2] = fin[p];
+            final_rgba[4 * p + 3] = 255;
+        }
+    if (d_ref_out) memcpy(d_ref_out, dr, sizeof(int32_t) * S);
+    if (d_tar_out) memcpy(d_tar_out, dt, sizeof(int32_t) * S);
+    free(vl); free(vr); free(hl); free(hr); free(el); free(er); free(kl); free(o1); free(o2); free(fin);
+    free(dr); free(dt);
+    return 0;
+}

@@ -48,6 +48,11 @@ def build(force: bool = False) -> None:
         subprocess.check_call(["make", "-s", "-C", _HERE, "all"])
 
 
+# refinement contraction policy (asw_oracle.c, oracle_refine): chosen against the
+# reference's device PNGs by tests/test_oracle_golden.py::test_refinement_policy
+REF_POL = 0
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -75,6 +80,8 @@ def lib():
     L.oracle_match_ex.restype = i
     L.oracle_raw_cost_tad.argtypes = [P, P, i, i, i, f, P]
     L.oracle_lab.argtypes = [P, i, i, P]
+    L.oracle_refine.argtypes = [P, P, i, i, i, i, i, i, P, P, P, P, P, P, P, P, P]
+    L.oracle_refine.restype = i
     L.oracle_support_lab.argtypes = [P, i, i, i, i, f, f, P]
     _lib = L
     return L
@@ -171,7 +178,7 @@ def consistency(code_ref, code_tar, conf_ref, conf_tar, D: int):
 
 def match(L: np.ndarray, R: np.ndarray, D: int, T: int, iters: int = 7, gc: float = GAMMA_C,
           gg: float = GAMMA_G, fma_mode: int = FMA_NUM, want_cost: bool = False, color_space: int = 0,
-          tad_tau: float = 765.0) -> dict:
+          tad_tau: float = 765.0, refine_iters: int = 0, refine_taps: int = 33, ref_pol: int = REF_POL) -> dict:
     """Full reference ASW pipeline (main.cpp:463-537) on host RGBA8 images [H][W][4]."""
     L = np.ascontiguousarray(L, np.uint8)
     R = np.ascontiguousarray(R, np.uint8)
@@ -182,12 +189,34 @@ def match(L: np.ndarray, R: np.ndarray, D: int, T: int, iters: int = 7, gc: floa
         "lr_rgba": np.empty((H, W, 4), np.uint8), "lr_red_rgba": np.empty((H, W, 4), np.uint8),
     }
     cost = np.empty((D, H, W), np.float32) if want_cost else None
+    if refine_iters and cost is None:
+        cost = np.empty((D, H, W), np.float32)
     rc = lib().oracle_match_ex(_p(L), _p(R), W, H, D, T, iters, gc, gg, fma_mode, color_space, tad_tau,
                             _p(out["d_ref"]), _p(out["conf_ref"]), _p(out["d_tar"]), _p(out["conf_tar"]),
                             _p(out["lr_rgba"]), _p(out["lr_red_rgba"]),
                             _p(cost) if cost is not None else None)
     if rc != 0:
         raise MemoryError("oracle_match failed to allocate")
-    if cost is not None:
+    if refine_iters:
+        out.update(refine(L, R, D, cost, out, refine_iters, refine_taps, ref_pol))
+    if want_cost:
         out["cost"] = cost
     return out
+
+
+def refine(L, R, D: int, cost, pre: dict, k: int, taps: int = 33, pol: int = REF_POL) -> dict:
+    """Refinement loop + 3x3 median (main.cpp:540-623) after a match() result `pre`."""
+    H, W = L.shape[:2]
+    conf_ref = np.ascontiguousarray(pre["conf_ref"], np.float32).copy()
+    conf_tar = np.ascontiguousarray(pre["conf_tar"], np.float32).copy()
+    est_left = np.ascontiguousarray(pre["lr_rgba"][..., 0])
+    est_right = code_u8(pre["d_tar"], D)
+    res = {"post_red_rgba": np.empty((H, W, 4), np.uint8), "final_rgba": np.empty((H, W, 4), np.uint8),
+           "ref_d_ref": np.empty((H, W), np.int32), "ref_d_tar": np.empty((H, W), np.int32)}
+    rc = lib().oracle_refine(_p(L), _p(R), W, H, D, k, taps, pol, _p(cost), _p(est_left), _p(est_right),
+                             _p(conf_ref), _p(conf_tar), _p(res["post_red_rgba"]), _p(res["final_rgba"]),
+                             _p(res["ref_d_ref"]), _p(res["ref_d_tar"]))
+    if rc != 0:
+        raise MemoryError("oracle_refine failed to allocate")
+    res["ref_conf_ref"], res["ref_conf_tar"] = conf_ref, conf_tar
+    return res
