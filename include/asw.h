@@ -114,10 +114,27 @@ int asw_support_lab(const asw_params *p, int dir, const float *lab, float *w, vo
 int asw_aggregate_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin,
                        float *cout, void *stream);
 
+/* Same pass with a cached denominator volume `den` ([H][W][Dp] float32, the cost
+ * layout).  The reference recomputes den = 1e-5 + sum_i wl_i*wr_i(xr) in every pass
+ * (K/asw_vcost_aggregation.cl:38, written to its dead asw_denom buffer); it does
+ * not depend on the cost, so ASW_DEN_WRITE stores it during a pass and
+ * ASW_DEN_READ reuses it in the later passes of the same direction (same
+ * supports).  Results are bit-identical in every mode. */
+#define ASW_DEN_NONE 0  /* compute den, do not touch `den` (may be NULL) */
+#define ASW_DEN_WRITE 1 /* compute den and store it to `den`            */
+#define ASW_DEN_READ 2  /* take den from `den` (written by a DEN_WRITE pass of this direction) */
+int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin,
+                           float *cout, float *den, int den_mode, void *stream);
+
 /* r x (V,H) ping-pong of main.cpp:486-515 on two caller buffers; the result
  * ends in `c0` (c0 holds the raw cost on entry, c1 is scratch). */
 int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
                   float *c0, float *c1, void *stream);
+/* asw_aggregate with cached denominators: den_v, den_h are two more [H][W][Dp]
+ * volumes (asw_cost_bytes each); the first iteration writes them, the other r-1
+ * read them.  den_v = den_h = NULL is asw_aggregate. */
+int asw_aggregate_den(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
+                      float *c0, float *c1, float *den_v, float *den_h, void *stream);
 
 /* replaces asw_WTA (K/asw_wta.cl:12-82), launched at main.cpp:517-526, for a context
  * that owns the whole disparity range: left first-argmin + confidence, the

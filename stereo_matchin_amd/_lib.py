@@ -31,6 +31,7 @@ ASW_E_UNSUPPORTED = -4
 
 DIR_V = 0
 DIR_H = 1
+DEN_NONE, DEN_WRITE, DEN_READ = 0, 1, 2  # ASW_DEN_* (cached aggregation denominator)
 COLOR_RGB = 0
 COLOR_LAB = 1
 LR_U8 = 0
@@ -116,7 +117,9 @@ SIGNATURES = {
     "asw_lab": (I, [PP, P, P, P]),
     "asw_support_lab": (I, [PP, I, P, P, P]),
     "asw_aggregate_pass": (I, [PP, I, P, P, P, P, P]),
+    "asw_aggregate_pass_den": (I, [PP, I, P, P, P, P, P, I, P]),
     "asw_aggregate": (I, [PP, P, P, P, P, P, P, P]),
+    "asw_aggregate_den": (I, [PP, P, P, P, P, P, P, P, P, P]),
     "asw_wta": (I, [PP, P, P, P, P, P, P, P, P]),
     "asw_consistency": (I, [PP, P, P, P, P, P, P, P, P, P]),
     "asw_wta_local": (I, [PP, P, P, P, P, P]),

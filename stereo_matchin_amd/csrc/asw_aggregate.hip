@@ -1,6 +1,7 @@
 // asw_aggregate.hip — dispatch of the aggregation passes over the compiled tap
-// counts; the kernels are in asw_aggregate_impl.h, instantiated one tap count per
-// translation unit (agg_t<T>.hip) so they compile in parallel.
+// counts and den modes; the kernels are in asw_aggregate_impl.h, instantiated one
+// (tap count, den mode) per translation unit (build/agg_t<T>_d<DM>.hip, generated
+// by the Makefile) so they compile in parallel.
 #include <hip/hip_runtime.h>
 
 #include "asw_common.h"
@@ -8,9 +9,16 @@
 namespace asw {
 namespace agg {
 int g_pass_variant = 0;
+template <int T, int DM>
+int launch_pass_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                   float *den, hipStream_t st);
 template <int T>
 int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                  hipStream_t st);
+                  float *den, int dm, hipStream_t st) {
+    if (dm == 1) return launch_pass_tm<T, 1>(p, dir, wl, wr, cin, cout, den, st);
+    if (dm == 2) return launch_pass_tm<T, 2>(p, dir, wl, wr, cin, cout, den, st);
+    return launch_pass_tm<T, 0>(p, dir, wl, wr, cin, cout, den, st);
+}
 }  // namespace agg
 
 int set_pass_variant(int v) {
@@ -20,11 +28,12 @@ int set_pass_variant(int v) {
 }
 
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                hipStream_t st) {
+                float *den, int dm, hipStream_t st) {
+    if (dm != 0 && !den) return ASW_E_INVALID;
     switch (p->taps) {
 #define ASW_CASE(TT) \
     case TT:         \
-        return agg::launch_pass_t<TT>(p, dir, wl, wr, cin, cout, st);
+        return agg::launch_pass_t<TT>(p, dir, wl, wr, cin, cout, den, dm, st);
         ASW_CASE(3)
         ASW_CASE(5)
         ASW_CASE(7)

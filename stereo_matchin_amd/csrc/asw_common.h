@@ -32,8 +32,9 @@ __host__ __device__ inline int code_u8(int d, int D) {
 void set_hip_error(hipError_t e);
 
 // one aggregation pass over every local plane (asw_aggregate.hip)
+// den/dm: cached-denominator mode (ASW_DEN_*; den = NULL with ASW_DEN_NONE)
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                hipStream_t st);
+                float *den, int dm, hipStream_t st);
 int set_pass_variant(int v);
 
 }  // namespace asw

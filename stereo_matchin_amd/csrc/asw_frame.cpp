@@ -21,6 +21,7 @@ struct asw_ctx {
     float *lab_l = nullptr, *lab_r = nullptr;  // float4 [H][W] (ASW_COLOR_LAB only)
     float *wvl = nullptr, *wvr = nullptr, *whl = nullptr, *whr = nullptr;  // [H][W][Tp]
     float *c0 = nullptr, *c1 = nullptr;                                    // [H][W][Dp]
+    float *den_v = nullptr, *den_h = nullptr;  // cached denominators [H][W][Dp] (iters >= 2)
     int32_t *d_ref = nullptr, *d_tar = nullptr;
     float *conf_ref = nullptr, *conf_tar = nullptr;
     uint8_t *code_ref = nullptr, *code_tar = nullptr;
@@ -78,6 +79,7 @@ int asw_destroy(asw_ctx *ctx) {
     if (!ctx) return ASW_OK;
     (void)hipSetDevice(ctx->device);
     void *bufs[] = {ctx->left, ctx->right, ctx->lut, ctx->lab_l, ctx->lab_r, ctx->wvl, ctx->wvr, ctx->whl, ctx->whr, ctx->c0, ctx->c1,
+                    ctx->den_v, ctx->den_h,
                     ctx->d_ref, ctx->d_tar, ctx->conf_ref, ctx->conf_tar, ctx->code_ref, ctx->code_tar, ctx->lr,
                     ctx->lr_red, ctx->disp};
     for (void *b : bufs)
@@ -123,6 +125,10 @@ int asw_create(const asw_params *p, int hip_device, asw_ctx **out) {
     chain(dev_alloc(&c->whr, asw_support_bytes(p)));
     chain(dev_alloc(&c->c0, asw_cost_bytes(p)));
     chain(dev_alloc(&c->c1, asw_cost_bytes(p)));
+    if (p->iters >= 2) {  // the den of a direction is written by its first pass and read by the r-1 others
+        chain(dev_alloc(&c->den_v, asw_cost_bytes(p)));
+        chain(dev_alloc(&c->den_h, asw_cost_bytes(p)));
+    }
     chain(dev_alloc(&c->d_ref, S * 4));
     chain(dev_alloc(&c->d_tar, S * 4));
     chain(dev_alloc(&c->conf_ref, S * 4));
@@ -188,9 +194,10 @@ int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
     HIPCHK(hipEventRecord(ev[3], st));
     if (timed) HIPCHK(hipEventRecord(ev[e_pass0], st));
     for (int it = 0; it < r; ++it) {
-        ASWCHK(asw_aggregate_pass(p, ASW_DIR_V, c->wvl, c->wvr, c->c0, c->c1, st));
+        const int dm = !c->den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
+        ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, c->wvl, c->wvr, c->c0, c->c1, c->den_v, dm, st));
         if (timed) HIPCHK(hipEventRecord(ev[e_pass0 + 2 * it + 1], st));
-        ASWCHK(asw_aggregate_pass(p, ASW_DIR_H, c->whl, c->whr, c->c1, c->c0, st));
+        ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, c->whl, c->whr, c->c1, c->c0, c->den_h, dm, st));
         if (timed) HIPCHK(hipEventRecord(ev[e_pass0 + 2 * it + 2], st));
     }
     ASWCHK(asw_wta(p, c->c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar, st));

@@ -559,16 +559,32 @@ int asw_aggregate_pass(const asw_params *p, int dir, const float *wl, const floa
     ASW_CHECK_PARAMS(p);
     if (!wl || !wr || !cin || !cout || cin == cout || (dir != ASW_DIR_V && dir != ASW_DIR_H))
         return ASW_E_INVALID;
-    return asw::launch_pass(p, dir, wl, wr, cin, cout, (hipStream_t)stream);
+    return asw::launch_pass(p, dir, wl, wr, cin, cout, nullptr, ASW_DEN_NONE, (hipStream_t)stream);
+}
+
+int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin,
+                           float *cout, float *den, int den_mode, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!wl || !wr || !cin || !cout || cin == cout || (dir != ASW_DIR_V && dir != ASW_DIR_H)) return ASW_E_INVALID;
+    if (den_mode < ASW_DEN_NONE || den_mode > ASW_DEN_READ) return ASW_E_INVALID;
+    if (den_mode != ASW_DEN_NONE && (!den || den == cin || den == cout)) return ASW_E_INVALID;
+    return asw::launch_pass(p, dir, wl, wr, cin, cout, den, den_mode, (hipStream_t)stream);
 }
 
 int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
                   float *c0, float *c1, void *stream) {
+    return asw_aggregate_den(p, wvl, wvr, whl, whr, c0, c1, nullptr, nullptr, stream);
+}
+
+int asw_aggregate_den(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
+                      float *c0, float *c1, float *den_v, float *den_h, void *stream) {
     ASW_CHECK_PARAMS(p);
+    const bool cached = den_v && den_h;
     for (int it = 0; it < p->iters; ++it) {
-        int s = asw_aggregate_pass(p, ASW_DIR_V, wvl, wvr, c0, c1, stream);
+        const int dm = !cached ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
+        int s = asw_aggregate_pass_den(p, ASW_DIR_V, wvl, wvr, c0, c1, den_v, dm, stream);
         if (s != ASW_OK) return s;
-        s = asw_aggregate_pass(p, ASW_DIR_H, whl, whr, c1, c0, stream);
+        s = asw_aggregate_pass_den(p, ASW_DIR_H, whl, whr, c1, c0, den_h, dm, stream);
         if (s != ASW_OK) return s;
     }
     return ASW_OK;

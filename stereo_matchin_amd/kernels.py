@@ -136,7 +136,7 @@ def asw_hSupport(p: AswParams, img: torch.Tensor, lut: torch.Tensor | None = Non
     return _support(p, DIR_H, img, lut, out)
 
 
-def _pass(p: AswParams, direction: int, supp_left, supp_right, cost_in, out):
+def _pass(p: AswParams, direction: int, supp_left, supp_right, cost_in, out, den=None, den_mode: int = 0):
     _expect(supp_left, support_shape(p), torch.float32, "supp_left")
     _expect(supp_right, support_shape(p), torch.float32, "supp_right")
     _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
@@ -145,20 +145,26 @@ def _pass(p: AswParams, direction: int, supp_left, supp_right, cost_in, out):
     _expect(out, cost_shape(p), torch.float32, "out")
     if out.data_ptr() == cost_in.data_ptr():
         raise ValueError("aggregation passes are out of place (cost_in != out)")
-    _lib.check(_lib.lib().asw_aggregate_pass(ctypes.byref(p), direction, _ptr(supp_left), _ptr(supp_right),
-                                             _ptr(cost_in), _ptr(out), _stream(cost_in.device)),
-               "asw_aggregate_pass")
+    if den_mode:
+        _expect(den, cost_shape(p), torch.float32, "den")
+    _lib.check(_lib.lib().asw_aggregate_pass_den(ctypes.byref(p), direction, _ptr(supp_left), _ptr(supp_right),
+                                                 _ptr(cost_in), _ptr(out), _ptr(den), den_mode,
+                                                 _stream(cost_in.device)),
+               "asw_aggregate_pass_den")
     return out
 
 
-def asw_vCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None):
-    """One vertical weighted-aggregation pass (K/asw_vcost_aggregation.cl:11-44)."""
-    return _pass(p, DIR_V, supp_left, supp_right, cost_in, out)
+def asw_vCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None, den=None, den_mode: int = 0):
+    """One vertical weighted-aggregation pass (K/asw_vcost_aggregation.cl:11-44).
+
+    ``den``/``den_mode`` (DEN_WRITE / DEN_READ): the cached-denominator volume, the
+    live form of the reference's write-only ``denom`` argument (``:38``)."""
+    return _pass(p, DIR_V, supp_left, supp_right, cost_in, out, den, den_mode)
 
 
-def asw_hCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None):
+def asw_hCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None, den=None, den_mode: int = 0):
     """One horizontal weighted-aggregation pass (K/asw_hcost_aggregation.cl:12-44)."""
-    return _pass(p, DIR_H, supp_left, supp_right, cost_in, out)
+    return _pass(p, DIR_H, supp_left, supp_right, cost_in, out, den, den_mode)
 
 
 def asw_WTA(p: AswParams, cost: torch.Tensor):

@@ -42,7 +42,13 @@ class MatchResult:
 
 
 class StereoMatcher:
-    def __init__(self, params: AswParams, device="cuda"):
+    """One GPU, one disparity shard: the buffers of main.cpp:434-457, allocated once.
+
+    ``den_cache`` (default on for r >= 2): keep the two aggregation denominators
+    (V, H) as volumes — written by the first pass of each direction, read by the
+    other r-1 (ASW_DEN_*); bit-identical results, 2 more cost-sized buffers."""
+
+    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True):
         st = _lib.params_check(params)
         if st != _lib.ASW_OK:
             raise _lib.AswError(st, "asw_params_check")
@@ -56,6 +62,10 @@ class StereoMatcher:
         self.whr = K.new_support(self.p, dev)
         self.c0 = K.new_cost(self.p, dev)
         self.c1 = K.new_cost(self.p, dev)
+        self.den_v = self.den_h = None
+        if den_cache and self.p.iters >= 2:
+            self.den_v = K.new_cost(self.p, dev)
+            self.den_h = K.new_cost(self.p, dev)
 
     # -- stages ---------------------------------------------------------------
     def raw_and_support(self, left: torch.Tensor, right: torch.Tensor):
@@ -77,11 +87,12 @@ class StereoMatcher:
     def aggregate(self, events: list | None = None):
         """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515)."""
         p = self.p
-        for _ in range(p.iters):
-            K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1)
+        for it in range(p.iters):
+            dm = _lib.DEN_NONE if self.den_v is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
+            K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1, den=self.den_v, den_mode=dm)
             if events is not None:
                 events.append(("v", _record()))
-            K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0)
+            K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0, den=self.den_h, den_mode=dm)
             if events is not None:
                 events.append(("h", _record()))
         return self.c0

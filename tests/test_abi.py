@@ -84,5 +84,9 @@ def test_stage_api_validates_before_launch(L):
     assert lib.asw_raw_cost(ctypes.byref(p), None, None, None, None) == L.ASW_E_INVALID
     assert lib.asw_aggregate_pass(ctypes.byref(p), 5, 1, 1, 1, 2, None) == L.ASW_E_INVALID
     assert lib.asw_aggregate_pass(ctypes.byref(p), 0, 1, 1, 1, 1, None) == L.ASW_E_INVALID  # in place
+    # cached-denominator pass: bad mode, missing den, den aliasing the output
+    assert lib.asw_aggregate_pass_den(ctypes.byref(p), 0, 1, 1, 1, 2, 3, 7, None) == L.ASW_E_INVALID
+    assert lib.asw_aggregate_pass_den(ctypes.byref(p), 0, 1, 1, 1, 2, None, L.DEN_READ, None) == L.ASW_E_INVALID
+    assert lib.asw_aggregate_pass_den(ctypes.byref(p), 0, 1, 1, 1, 2, 2, L.DEN_WRITE, None) == L.ASW_E_INVALID
     p.d_end = 30
     assert lib.asw_wta(ctypes.byref(p), 1, 1, 1, 1, 1, None, None, None) == L.ASW_E_INVALID  # sharded

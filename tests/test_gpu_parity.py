@@ -131,6 +131,33 @@ def test_single_pass_sharded_planes(gpu, oracle, direction):
     assert np.array_equal(got, want)
 
 
+# cached denominators: a DEN_WRITE pass on one cost volume, then a DEN_READ pass on
+# another with the same supports, each bit-exact against the oracle's full pass
+@pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35, 51])
+@pytest.mark.parametrize("direction", [0, 1])
+@pytest.mark.parametrize("H,W,D,d0,d1", [(37, 91, 70, 0, 70), (23, 150, 200, 70, 135)])
+def test_den_cache_write_then_read(gpu, oracle, T, direction, H, W, D, d0, d1):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    Lh, Rh = _rand_pair(T * 3 + direction + W, H, W, shift=6)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
+    Dp = K.cost_shape(p)[2]
+    rng = np.random.default_rng(T + D)
+    sl, sr = oracle.support(Lh, T, direction), oracle.support(Rh, T, direction)
+    f = K.asw_vSupport if direction == 0 else K.asw_hSupport
+    g = K.asw_vCostAggregation if direction == 0 else K.asw_hCostAggregation
+    wl, wr = f(p, _t(Lh, gpu)), f(p, _t(Rh, gpu))
+    den = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+    for mode in (_lib.DEN_WRITE, _lib.DEN_READ):
+        cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+        want = oracle.aggregate_pass(sl, sr, cin, T, direction, d0=d0, d1=d1, plane_base=d0)
+        out = g(p, wl, wr, _t(pixel_major(cin, Dp), gpu), den=den, den_mode=mode)
+        got = plane_major(_np(out), d1 - d0)
+        assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
+
+
 # every compiled pass variant (asw_tune_set): block shapes, 8-wave V, and the
 # diagonal-pair H kernel (Dp % 128 == 0), on shapes that hit segment / row edges
 @pytest.mark.parametrize("variant", [0, 2, 4, 8, 16])

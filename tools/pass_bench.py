@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--workload", default="c4")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="0,1,2,3,4,5,8,9")
+    ap.add_argument("--den", action="store_true", help="also time the cached-denominator modes (write, read)")
     args = ap.parse_args()
     W, H, D, T, iters, lr, desc = WORKLOADS[args.workload]
     dev = torch.device("cuda:0")
@@ -44,33 +45,38 @@ def main():
     cin = m.c0
     out = torch.empty_like(cin)
     variants = [int(v) for v in args.variants.split(",")]
+    modes = [0, 1, 2] if args.den else [0]  # ASW_DEN_NONE / WRITE / READ
+    dens = {"v": torch.empty_like(cin), "h": torch.empty_like(cin)} if args.den else {}
     lib = _lib.lib()
     S = W * H
     nbytes = 8 * D * S + 8 * T * S
     ref = {}
-    times = {(v, d): [] for v in variants for d in "vh"}
+    times = {(v, d, dm): [] for v in variants for d in "vh" for dm in modes}
     for rep in range(args.reps + 1):
         for v in variants:
             lib.asw_tune_set(1, v)
             for d, fn, wl, wr in (("v", K.asw_vCostAggregation, m.wvl, m.wvr),
                                   ("h", K.asw_hCostAggregation, m.whl, m.whr)):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                fn(p, wl, wr, cin, out=out)
-                e1.record()
-                torch.cuda.synchronize()
-                if rep == 0:
-                    if v == variants[0]:
-                        ref[d] = out.clone()
-                    elif not torch.equal(out, ref[d]):
-                        print(json.dumps({"variant": v, "dir": d, "error": "output differs from variant 0"}))
-                else:
-                    times[(v, d)].append(e0.elapsed_time(e1))
+                for dm in modes:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    fn(p, wl, wr, cin, out=out, den=dens.get(d), den_mode=dm)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    if rep == 0:
+                        if v == variants[0] and dm == 0:
+                            ref[d] = out.clone()
+                        elif not torch.equal(out, ref[d]):
+                            print(json.dumps({"variant": v, "dir": d, "den_mode": dm,
+                                              "error": "output differs from variant 0"}))
+                    else:
+                        times[(v, d, dm)].append(e0.elapsed_time(e1))
     lib.asw_tune_set(1, 0)
-    for (v, d), ts in times.items():
+    for (v, d, dm), ts in times.items():
         med = float(np.median(ts))
-        print(json.dumps({"workload": args.workload, "variant": v, "dir": d, "ms_median": round(med, 4),
-                          "ms_min": round(min(ts), 4), "GBps": round(nbytes / med / 1e6, 1),
+        print(json.dumps({"workload": args.workload, "variant": v, "dir": d, "den_mode": dm,
+                          "ms_median": round(med, 4), "ms_min": round(min(ts), 4),
+                          "GBps": round(nbytes / med / 1e6, 1),
                           "frac_of_8TBps": round(nbytes / med / 1e6 / 8000, 4)}))
 
 
