@@ -165,10 +165,61 @@ int asw_wta_finalize(const asw_params *p, const int64_t *key, const float *m2, c
                      const float *t2, int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar,
                      uint8_t *code_ref, uint8_t *code_tar, void *stream);
 
+/* ---- refinement loop (main.cpp:540-623): k x (asw_ref_v, asw_ref_h on both views,
+ * asw_WTA_REF, Constistency), then the 3x3 Median -> asw_disparity.png ----
+ * Whole-volume contexts only (d_begin = 0, d_end = ndisp), ndisp <= 256, ASW_LR_U8:
+ * the loop feeds disparities back through the reference's 8-bit codes. */
+typedef struct asw_refine_params {
+    int iters;      /* k refinement iterations (main.cpp:178: 6)                      */
+    int taps;       /* window of asw_ref_v / asw_ref_h (K/asw_refinement_v.cl:33: 33)  */
+    float gamma_c;  /* 10.94 (K/asw_refinement_v.cl:6)                                 */
+    float gamma_g;  /* 118.78 (K/asw_refinement_v.cl:7)                                */
+    float alpha;    /* penalty slope 0.085 (K/asw_wta_ref.cl:28); only 0.085 is built  */
+} asw_refine_params;
+
+void asw_refine_params_default(asw_refine_params *rp);
+int asw_refine_params_check(const asw_params *p, const asw_refine_params *rp);
+size_t asw_refine_lut_bytes(const asw_refine_params *rp);
+/* weight table of the refinement kernels (asw_support_lut with the refinement falloffs) */
+int asw_refine_lut(const asw_params *p, const asw_refine_params *rp, float *lut, void *stream);
+
+/* replaces asw_ref_v (K/asw_refinement_v.cl:13-51), main.cpp:547-558.  est: u8
+ * disparity codes read at `est_stride` bytes per pixel (4 = channel 0 of an RGBA8
+ * image such as consistency_error, 1 = a plain code map).  out: [2][H][W] f32,
+ * plane 0 = the refined disparity estimate num/den, plane 1 = den. */
+int asw_ref_v(const asw_params *p, const asw_refine_params *rp, const uint8_t *img_rgba, const uint8_t *est,
+              int est_stride, const float *conf, const float *lut, float *out, void *stream);
+/* replaces asw_ref_h (K/asw_refinement_h.cl:16-53), main.cpp:561-573; in/out [2][H][W]. */
+int asw_ref_h(const asw_params *p, const asw_refine_params *rp, const uint8_t *img_rgba, const float *conf,
+              const float *in, const float *lut, float *out, void *stream);
+/* replaces asw_WTA_REF (K/asw_wta_ref.cl:2-68), main.cpp:576-586: first-argmin of
+ * 0.085*den*|val - d| + C[d] (left) and the same along the target diagonal.
+ * As the reference: conf_ref receives the TARGET confidence (its second store to
+ * `confidence`), the target confidence array is not written. */
+int asw_wta_ref(const asw_params *p, const float *cost, const float *ref_l, const float *ref_r, int32_t *d_ref,
+                int32_t *d_tar, float *conf_ref, uint8_t *code_ref, uint8_t *code_tar, void *stream);
+/* replaces Median (K/median.cl:58-88), main.cpp:615-617: 3x3 median of u8 codes
+ * (stride 1 or 4 bytes per pixel), clamped borders; out = grey RGBA8. */
+int asw_median3(const asw_params *p, const uint8_t *codes, int stride, uint8_t *out_rgba, void *stream);
+
+/* The whole loop on device buffers.  In: the final aggregated volume `cost`, the
+ * pre-refinement consistency image est_left_rgba (asw_consistency's out_rgba) and
+ * target codes code_tar (asw_wta's), confidences after that consistency check.
+ * All four are updated in place, as the reference's buffers are.  Out (any may be
+ * NULL): post_red_rgba (asw_consistency_post-reff.png, written when iters > 0),
+ * final_rgba (asw_disparity.png), d_ref / d_tar of the last asw_WTA_REF.
+ * workspace: asw_refine_workspace_bytes() of device memory. */
+size_t asw_refine_workspace_bytes(const asw_params *p, const asw_refine_params *rp);
+int asw_refine(const asw_params *p, const asw_refine_params *rp, const uint8_t *left_rgba, const uint8_t *right_rgba,
+               const float *cost, uint8_t *est_left_rgba, uint8_t *code_tar, float *conf_ref, float *conf_tar,
+               void *workspace, uint8_t *post_red_rgba, uint8_t *final_rgba, int32_t *d_ref, int32_t *d_tar,
+               void *stream);
+
 /* tuning hook (benchmarks / kernel experiments): selects among compiled kernel
  * variants; returns the previous value, or ASW_E_INVALID for an unknown key.
  * Every variant computes bit-identical results. */
 #define ASW_TUNE_PASS_VARIANT 1
+#define ASW_TUNE_WTA_VARIANT 2 /* 0: lane-per-pixel scan (default), 1: wave-per-pixel reduction */
 int asw_tune_set(int key, int value);
 
 /* ---------------- FRAME API (host pointers, synchronous) ---------------- */
@@ -182,11 +233,14 @@ typedef struct asw_outputs { /* caller-owned host arrays; any may be NULL */
     uint8_t *lr_rgba;        /* [H][W][4] consistency output ("consistency_error") */
     uint8_t *lr_red_rgba;    /* [H][W][4] asw_consistency_pre-reff.png image    */
     float *cost;             /* [H][W][Dp] final aggregated volume (optional)   */
+    uint8_t *final_rgba;     /* [H][W][4] asw_disparity.png (refinement on)     */
+    uint8_t *post_red_rgba;  /* [H][W][4] asw_consistency_post-reff.png (refinement on) */
 } asw_outputs;
 
 typedef struct asw_timings { /* milliseconds from HIP events, columns of main.cpp:181 */
     double raw_cost, support, v_pass_mean, h_pass_mean, aggregation_total, wta, consistency, total;
     double h2d, d2h;
+    double refine;           /* refinement loop + median (0 when off) */
 } asw_timings;
 
 /* marketing name of a HIP device (the reference names its TSV after the OpenCL
@@ -198,6 +252,10 @@ int asw_create(const asw_params *p, int hip_device, asw_ctx **out);
 int asw_destroy(asw_ctx *ctx);
 int asw_match(asw_ctx *ctx, const uint8_t *left_rgba, const uint8_t *right_rgba, asw_outputs *out,
               asw_timings *t);
+/* turn the refinement loop on for later asw_match calls (rp = NULL or iters = 0:
+ * off, the default).  Needs lr_check; asw_match then fills final_rgba /
+ * post_red_rgba and leaves lr_rgba as the pre-refinement consistency image. */
+int asw_set_refine(asw_ctx *ctx, const asw_refine_params *rp);
 
 #ifdef __cplusplus
 }

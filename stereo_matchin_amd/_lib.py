@@ -82,13 +82,21 @@ class AswOutputs(ctypes.Structure):
         ("conf_ref", ctypes.c_void_p), ("conf_tar", ctypes.c_void_p),
         ("disp_rgba", ctypes.c_void_p), ("lr_rgba", ctypes.c_void_p),
         ("lr_red_rgba", ctypes.c_void_p), ("cost", ctypes.c_void_p),
+        ("final_rgba", ctypes.c_void_p), ("post_red_rgba", ctypes.c_void_p),
     ]
+
+
+class AswRefineParams(ctypes.Structure):
+    """Mirror of ``asw_refine_params`` (include/asw.h)."""
+
+    _fields_ = [("iters", ctypes.c_int), ("taps", ctypes.c_int), ("gamma_c", ctypes.c_float),
+                ("gamma_g", ctypes.c_float), ("alpha", ctypes.c_float)]
 
 
 class AswTimings(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in (
         "raw_cost", "support", "v_pass_mean", "h_pass_mean", "aggregation_total", "wta",
-        "consistency", "total", "h2d", "d2h")]
+        "consistency", "total", "h2d", "d2h", "refine")]
 
 
 _lib = None
@@ -96,6 +104,7 @@ _load_error: Exception | None = None
 
 P = ctypes.c_void_p
 PP = ctypes.POINTER(AswParams)
+RP = ctypes.POINTER(AswRefineParams)
 I = ctypes.c_int
 
 # name -> (restype, argtypes).  Every function declared in include/asw.h.
@@ -126,6 +135,17 @@ SIGNATURES = {
     "asw_wta_target_local": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_second": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_finalize": (I, [PP, P, P, P, P, P, P, P, P, P, P, P]),
+    "asw_refine_params_default": (None, [RP]),
+    "asw_refine_params_check": (I, [PP, RP]),
+    "asw_refine_lut_bytes": (ctypes.c_size_t, [RP]),
+    "asw_refine_lut": (I, [PP, RP, P, P]),
+    "asw_ref_v": (I, [PP, RP, P, P, I, P, P, P, P]),
+    "asw_ref_h": (I, [PP, RP, P, P, P, P, P, P]),
+    "asw_wta_ref": (I, [PP, P, P, P, P, P, P, P, P, P]),
+    "asw_median3": (I, [PP, P, I, P, P]),
+    "asw_refine_workspace_bytes": (ctypes.c_size_t, [PP, RP]),
+    "asw_refine": (I, [PP, RP, P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "asw_set_refine": (I, [P, RP]),
     "asw_tune_set": (I, [I, I]),
     "asw_device_name": (I, [I, ctypes.c_char_p, I]),
     "asw_create": (I, [PP, I, ctypes.POINTER(P)]),
@@ -190,6 +210,17 @@ def default_params(width: int = 0, height: int = 0, **kw) -> AswParams:
             raise TypeError(f"unknown asw_params field {k!r}")
         setattr(p, k, v)
     return p
+
+
+def default_refine_params(**kw) -> AswRefineParams:
+    """Reference refinement settings (k = 6, 33 taps, 10.94 / 118.78, 0.085), overridable."""
+    rp = AswRefineParams()
+    _load().asw_refine_params_default(ctypes.byref(rp))
+    for k, v in kw.items():
+        if not hasattr(rp, k):
+            raise TypeError(f"unknown asw_refine_params field {k!r}")
+        setattr(rp, k, v)
+    return rp
 
 
 def disp_pitch(p: AswParams) -> int:

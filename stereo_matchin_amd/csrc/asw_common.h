@@ -37,4 +37,9 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
                 float *den, int dm, hipStream_t st);
 int set_pass_variant(int v);
 
+// lane-per-pixel WTA scan (asw_refine.hip): mode 0 = asw_WTA, 1 = asw_WTA_REF
+int launch_wta_scan(const asw_params *p, int mode, const float *cost, const float *ref_l, const float *ref_r,
+                    int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar, uint8_t *code_ref,
+                    uint8_t *code_tar, hipStream_t st);
+
 }  // namespace asw

@@ -26,6 +26,12 @@ struct asw_ctx {
     float *conf_ref = nullptr, *conf_tar = nullptr;
     uint8_t *code_ref = nullptr, *code_tar = nullptr;
     uint8_t *lr = nullptr, *lr_red = nullptr, *disp = nullptr;  // RGBA8
+    // refinement loop (asw_set_refine): parameters, workspace, its estimate image
+    // (a copy of lr, refined in place) and outputs
+    asw_refine_params rp{};
+    bool refine = false;
+    void *rws = nullptr;
+    uint8_t *est = nullptr, *post_red = nullptr, *final_rgba = nullptr;  // RGBA8
     hipEvent_t ev[32] = {};
 };
 
@@ -81,7 +87,7 @@ int asw_destroy(asw_ctx *ctx) {
     void *bufs[] = {ctx->left, ctx->right, ctx->lut, ctx->lab_l, ctx->lab_r, ctx->wvl, ctx->wvr, ctx->whl, ctx->whr, ctx->c0, ctx->c1,
                     ctx->den_v, ctx->den_h,
                     ctx->d_ref, ctx->d_tar, ctx->conf_ref, ctx->conf_tar, ctx->code_ref, ctx->code_tar, ctx->lr,
-                    ctx->lr_red, ctx->disp};
+                    ctx->lr_red, ctx->disp, ctx->rws, ctx->est, ctx->post_red, ctx->final_rgba};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t &e : ctx->ev)
@@ -157,6 +163,29 @@ int asw_device_name(int hip_device, char *buf, int len) {
     return ASW_OK;
 }
 
+int asw_set_refine(asw_ctx *c, const asw_refine_params *rp) {
+    if (!c) return ASW_E_INVALID;
+    if (!rp || rp->iters <= 0) {
+        c->refine = false;
+        return ASW_OK;
+    }
+    const int s = asw_refine_params_check(&c->p, rp);
+    if (s != ASW_OK) return s;
+    if (!c->p.lr_check) return ASW_E_INVALID;  // the loop starts from the consistency image
+    HIPCHK(hipSetDevice(c->device));
+    const size_t S = (size_t)c->p.width * c->p.height;
+    const size_t ws = asw_refine_workspace_bytes(&c->p, rp);
+    if (c->rws) (void)hipFree(c->rws);
+    c->rws = nullptr;
+    ASWCHK(dev_alloc(&c->rws, ws));
+    if (!c->est) ASWCHK(dev_alloc(&c->est, S * 4));
+    if (!c->post_red) ASWCHK(dev_alloc(&c->post_red, S * 4));
+    if (!c->final_rgba) ASWCHK(dev_alloc(&c->final_rgba, S * 4));
+    c->rp = *rp;
+    c->refine = true;
+    return ASW_OK;
+}
+
 int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, asw_outputs *o, asw_timings *t) {
     if (!c || !left_rgba || !right_rgba) return ASW_E_INVALID;
     HIPCHK(hipSetDevice(c->device));
@@ -168,7 +197,7 @@ int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
     // event slots: 0 h2d start, 1 raw start, 2 raw end / support start, 3 support end,
     // 4.. per pass (2r+1 slots), then wta end, consistency end, d2h end.
     const int e_pass0 = 4;
-    const int e_wta = e_pass0 + 2 * r + 1 > 28 ? -1 : e_pass0 + 2 * r + 1;
+    const int e_wta = e_pass0 + 2 * r + 1 > 28 ? -1 : e_pass0 + 2 * r + 1;  // slots up to e_wta + 3 = 31
     const bool timed = e_wta >= 0;
 
     HIPCHK(hipEventRecord(ev[0], st));
@@ -209,6 +238,13 @@ int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
         ASWCHK(asw_consistency(p, c->d_ref, c->d_tar, c->code_ref, c->code_tar, c->conf_ref, c->conf_tar, c->lr,
                                c->lr_red, st));
     if (timed) HIPCHK(hipEventRecord(ev[e_wta + 1], st));
+    const bool refine = c->refine && p->lr_check;
+    if (refine) {  // main.cpp:540-617 on a copy of consistency_error
+        HIPCHK(hipMemcpyAsync(c->est, c->lr, S * 4, hipMemcpyDeviceToDevice, st));
+        ASWCHK(asw_refine(p, &c->rp, c->left, c->right, c->c0, c->est, c->code_tar, c->conf_ref, c->conf_tar, c->rws,
+                          c->post_red, c->final_rgba, nullptr, nullptr, st));
+    }
+    if (timed) HIPCHK(hipEventRecord(ev[e_wta + 2], st));
     if (o) {
         if (o->d_ref) HIPCHK(hipMemcpyAsync(o->d_ref, c->d_ref, S * 4, hipMemcpyDeviceToHost, st));
         if (o->d_tar) HIPCHK(hipMemcpyAsync(o->d_tar, c->d_tar, S * 4, hipMemcpyDeviceToHost, st));
@@ -219,8 +255,12 @@ int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
         if (o->lr_red_rgba && p->lr_check)
             HIPCHK(hipMemcpyAsync(o->lr_red_rgba, c->lr_red, S * 4, hipMemcpyDeviceToHost, st));
         if (o->cost) HIPCHK(hipMemcpyAsync(o->cost, c->c0, asw_cost_bytes(p), hipMemcpyDeviceToHost, st));
+        if (o->final_rgba && refine)
+            HIPCHK(hipMemcpyAsync(o->final_rgba, c->final_rgba, S * 4, hipMemcpyDeviceToHost, st));
+        if (o->post_red_rgba && refine && c->rp.iters > 0)
+            HIPCHK(hipMemcpyAsync(o->post_red_rgba, c->post_red, S * 4, hipMemcpyDeviceToHost, st));
     }
-    if (timed) HIPCHK(hipEventRecord(ev[e_wta + 2], st));
+    if (timed) HIPCHK(hipEventRecord(ev[e_wta + 3], st));
     HIPCHK(hipStreamSynchronize(st));
     if (t && timed) {
         std::memset(t, 0, sizeof(*t));
@@ -238,7 +278,8 @@ int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
         t->wta = ms_between(ev[e_pass0 + 2 * r], ev[e_wta]);
         t->consistency = ms_between(ev[e_wta], ev[e_wta + 1]);
         t->total = ms_between(ev[1], ev[e_wta + 1]);
-        t->d2h = ms_between(ev[e_wta + 1], ev[e_wta + 2]);
+        t->refine = refine ? ms_between(ev[e_wta + 1], ev[e_wta + 2]) : 0.0;
+        t->d2h = ms_between(ev[e_wta + 2], ev[e_wta + 3]);
     }
     return ASW_OK;
 }

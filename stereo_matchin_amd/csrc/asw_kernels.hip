@@ -432,8 +432,15 @@ extern "C" {
 
 int asw_abi_version(void) { return 1; }
 
+static int g_wta_variant = 0;
+
 int asw_tune_set(int key, int value) {
     if (key == ASW_TUNE_PASS_VARIANT) return asw::set_pass_variant(value);
+    if (key == ASW_TUNE_WTA_VARIANT) {
+        const int old = g_wta_variant;
+        g_wta_variant = value;
+        return old;
+    }
     return ASW_E_INVALID;
 }
 
@@ -595,6 +602,9 @@ int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_
     ASW_CHECK_PARAMS(p);
     if (p->d_begin != 0 || d_end_of(p) != p->ndisp) return ASW_E_INVALID;  // sharded: use asw_wta_local & co.
     if (!cost || !d_ref || !conf_ref || !d_tar || !conf_tar) return ASW_E_INVALID;
+    if (g_wta_variant == 0)
+        return asw::launch_wta_scan(p, 0, cost, nullptr, nullptr, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar,
+                                    (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
     const int bpx = (int)(((n + 3) / 4 + 7) / 8);
     hipLaunchKernelGGL(k_wta, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost, p->width,

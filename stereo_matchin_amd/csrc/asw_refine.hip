@@ -1,0 +1,408 @@
+// asw_refine.hip — the lane-per-pixel WTA scan (asw_WTA and asw_WTA_REF) and the
+// refinement loop of the reference (main.cpp:540-623): asw_ref_v, asw_ref_h,
+// asw_WTA_REF, Constistency (asw_consistency), then the 3x3 Median.
+//
+// WTA scan (K/asw_wta.cl:25-67, K/asw_wta_ref.cl:21-57).  The reference scans d
+// sequentially per pixel with strict '<'; here each LANE owns one pixel and runs
+// that same sequential scan, so ties, the multiset second minimum and the
+// 100000 sentinels are reproduced by construction (no cross-lane reduction).
+// The volume is pixel-major [H][W][Dp]: a wave's 64 pixels are 64 rows of Dp
+// floats, so a chunk of 32 planes is loaded coalesced (8 lanes per pixel, one
+// float4 each) and transposed through a private LDS tile [64][33] (row pitch 33:
+// the 32 lanes of a ds_read_b32 group hit 32 distinct banks, and so do the
+// ds_write_b32 of the transpose).  The next chunk's loads are in flight while
+// the current one is scanned.  The target scan (the bresenham diagonal
+// C[b][y][max(0,x-i)], b = md + max(0,x-i) - x) is a per-lane gather of the
+// row the wave just streamed (L2-resident).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "asw_common.h"
+
+namespace asw {
+namespace {
+
+constexpr float kSentinel = 100000.0f;  // K/asw_wta.cl:25-26, K/asw_wta_ref.cl:20-21
+constexpr int kChunk = 32;              // planes per transposed chunk
+constexpr int kTilePitch = kChunk + 1;
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// one element of the sequential scan (K/asw_wta.cl:43-46 order)
+__device__ __forceinline__ void scan_step(float t, int d, float &cur, float &last, int &md) {
+    last = t < last ? t : last;
+    md = t < cur ? d : md;
+    last = t < cur ? cur : last;
+    cur = t < cur ? t : cur;
+}
+
+// K/asw_wta_ref.cl:28: 0.085f * den * fabs(val - i) + cost, left to right, uncontracted
+__device__ __forceinline__ float penalty(float a, float val, int i, float c) {
+    const float b = fabsf(val - (float)i);
+    return a * b + c;
+}
+
+// MODE 0: asw_WTA — scanned value = cost; outputs d_ref, conf_ref, d_tar, conf_tar, codes.
+// MODE 1: asw_WTA_REF — scanned value = penalty + cost with the refinement
+//   estimates ref_l / ref_r ([2][S]: value plane, den plane); outputs d_ref,
+//   d_tar, codes, and conf_ref <- the TARGET confidence (the kernel's second,
+//   overwriting store to `confidence`, K/asw_wta_ref.cl:64-66); conf_tar untouched.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost, int W, int H, int Dp, int D,
+                                                  const float *__restrict__ ref_l, const float *__restrict__ ref_r,
+                                                  int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
+                                                  int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
+                                                  uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar,
+                                                  int nwaves) {
+    using f4 = float __attribute__((ext_vector_type(4)));
+    __shared__ float tile_all[4][64 * kTilePitch];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    // XCD-aware: blocks b, b+8, b+16, ... run on one XCD; give each XCD a
+    // contiguous range of waves so its target gathers hit rows its L2 just streamed
+    const int per_xcd = (nwaves / 4 + 7) / 8;
+    const int wave_id = ((blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3)) * 4 + wv;
+    if (wave_id >= nwaves) return;
+    float *tile = tile_all[wv];
+    const long long S = (long long)W * H;
+    const long long p0 = (long long)wave_id * 64;
+    const long long p = p0 + lane;
+    const bool live = p < S;
+
+    // chunk loader: instruction j (0..7) of lane l covers pixel j*8 + l/8, planes (l%8)*4..+3
+    const int sub = lane & 7, prow = lane >> 3;
+    const float *src[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const long long pp = min(p0 + j * 8 + prow, S - 1);
+        src[j] = cost + pp * Dp + sub * 4;
+    }
+    f4 buf[8];
+    const int nchunk = (D + kChunk - 1) / kChunk;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) buf[j] = *reinterpret_cast<const f4 *>(src[j]);
+
+    float a = 0.0f, val = 0.0f;
+    if constexpr (MODE == 1) {
+        const long long pq = live ? p : S - 1;
+        a = 0.085f * ref_l[S + pq];
+        val = ref_l[pq];
+    }
+    float cur = kSentinel, last = kSentinel;
+    int md = 0;
+    for (int c = 0; c < nchunk; ++c) {
+        // transpose the chunk into the wave's tile (row = pixel)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float *row = tile + (j * 8 + prow) * kTilePitch + sub * 4;
+            row[0] = buf[j].x;
+            row[1] = buf[j].y;
+            row[2] = buf[j].z;
+            row[3] = buf[j].w;
+        }
+        if (c + 1 < nchunk) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) buf[j] = *reinterpret_cast<const f4 *>(src[j] + (c + 1) * kChunk);
+        }
+        __builtin_amdgcn_wave_barrier();
+        const float *mine = tile + lane * kTilePitch;
+        const int d0 = c * kChunk;
+        if (d0 + kChunk <= D) {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) {
+                float t = mine[k];
+                if constexpr (MODE == 1) t = penalty(a, val, d0 + k, t);
+                scan_step(t, d0 + k, cur, last, md);
+            }
+        } else {
+            for (int k = 0; k < D - d0; ++k) {
+                float t = mine[k];
+                if constexpr (MODE == 1) t = penalty(a, val, d0 + k, t);
+                scan_step(t, d0 + k, cur, last, md);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (!live) return;
+
+    // target scan (K/asw_wta.cl:50-67, K/asw_wta_ref.cl:39-57)
+    const int x = (int)(p % W), y = (int)(p / W);
+    float at = 0.0f, valt = 0.0f;
+    if constexpr (MODE == 1) {
+        at = 0.085f * ref_r[S + p];
+        valt = ref_r[p];
+    }
+    const float *crow = cost + (long long)y * W * Dp;
+    float cur_t = kSentinel, last_t = kSentinel;
+    int mdr = md;
+    for (int i = 0; i < md; ++i) {
+        const int xq = x - i < 0 ? 0 : x - i;
+        const int b = md + xq - x;
+        float t = crow[(long long)xq * Dp + b];
+        if constexpr (MODE == 1) t = penalty(at, valt, i, t);
+        scan_step(t, b, cur_t, last_t, mdr);
+    }
+    d_ref[p] = md;
+    d_tar[p] = mdr;
+    if constexpr (MODE == 0) {
+        conf_ref[p] = (last - cur) / last;
+        conf_tar[p] = (last_t - cur_t) / last_t;
+    } else {
+        conf_ref[p] = (last_t - cur_t) / last_t;
+    }
+    if (code_ref) code_ref[p] = (uint8_t)code_u8(md, D);
+    if (code_tar) code_tar[p] = (uint8_t)code_u8(mdr, D);
+}
+
+// asw_ref_v (K/asw_refinement_v.cl:13-51): per pixel, over the Tr vertical taps
+// q = (x, clamp(y+i-Rr)): w = exp(-SAD/10.94 - |dy|/118.78) (LUT), D = (code/255)*(ndisp-1),
+// F = conf[q]; t = w*F; num += t*D; den += t  (num = den = 1e-5 on entry).
+// out = [num/den plane][den plane].  est is a u8 code image read with a stride
+// (4: channel 0 of an RGBA8 image, as read_imagef(...).x does; 1: plain codes).
+__global__ __launch_bounds__(256) void k_ref_v(const uchar4 *__restrict__ img, const uint8_t *__restrict__ est,
+                                               int est_stride, const float *__restrict__ conf,
+                                               const float *__restrict__ lut, int W, int H, int Tr, float scale,
+                                               float *__restrict__ out) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    const int Rr = Tr / 2;
+    const long long S = (long long)W * H;
+    const uchar4 pc = img[(long long)y * W + x];
+    float num = 0.00001f, den = 0.00001f;
+    for (int i = 0; i < Tr; ++i) {
+        const int qy = clampi(y + i - Rr, 0, H - 1);
+        const long long q = (long long)qy * W + x;
+        const uchar4 qc = img[q];
+        const int sad = abs((int)pc.x - qc.x) + abs((int)pc.y - qc.y) + abs((int)pc.z - qc.z);
+        const int dist = y > qy ? y - qy : qy - y;
+        const float w = lut[dist * kLutWidth + sad];
+        const float Dv = ((float)est[q * est_stride] / 255.0f) * scale;
+        const float t = w * conf[q];
+        num = num + t * Dv;
+        den = den + t;
+    }
+    out[(long long)y * W + x] = num / den;
+    out[S + (long long)y * W + x] = den;
+}
+
+// asw_ref_h (K/asw_refinement_h.cl:16-53): over the Tr horizontal taps
+// q = (clamp(x+i-Rr), y): t = w*F; num += (t*r)*n; den += t*n with r, n the value
+// and den planes of asw_ref_v's output.
+__global__ __launch_bounds__(256) void k_ref_h(const uchar4 *__restrict__ img, const float *__restrict__ conf,
+                                               const float *__restrict__ in, const float *__restrict__ lut, int W,
+                                               int H, int Tr, float *__restrict__ out) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    const int Rr = Tr / 2;
+    const long long S = (long long)W * H;
+    const long long row = (long long)y * W;
+    const uchar4 pc = img[row + x];
+    float num = 0.00001f, den = 0.00001f;
+    for (int i = 0; i < Tr; ++i) {
+        const int qx = clampi(x + i - Rr, 0, W - 1);
+        const long long q = row + qx;
+        const uchar4 qc = img[q];
+        const int sad = abs((int)pc.x - qc.x) + abs((int)pc.y - qc.y) + abs((int)pc.z - qc.z);
+        const int dist = x > qx ? x - qx : qx - x;
+        const float w = lut[dist * kLutWidth + sad];
+        const float t = w * conf[q];
+        const float tr = t * in[q];
+        const float n = in[S + q];
+        num = num + tr * n;
+        den = den + t * n;
+    }
+    out[row + x] = num / den;
+    out[S + row + x] = den;
+}
+
+// Median (K/median.cl:58-88): the min/max network there yields the exact median
+// of the 9 clamped neighbours; here a 19-exchange sorting network on the codes.
+__device__ __forceinline__ void cswap(int &a, int &b) {
+    const int lo = min(a, b), hi = max(a, b);
+    a = lo;
+    b = hi;
+}
+
+__global__ __launch_bounds__(256) void k_median3(const uint8_t *__restrict__ in, int in_stride, int W, int H,
+                                                 uchar4 *__restrict__ out) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    int v[9];
+    int n = 0;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx)
+            v[n++] = in[((long long)clampi(y + dy, 0, H - 1) * W + clampi(x + dx, 0, W - 1)) * in_stride];
+    // Paeth's median-of-9 exchange network
+    cswap(v[1], v[2]); cswap(v[4], v[5]); cswap(v[7], v[8]);
+    cswap(v[0], v[1]); cswap(v[3], v[4]); cswap(v[6], v[7]);
+    cswap(v[1], v[2]); cswap(v[4], v[5]); cswap(v[7], v[8]);
+    cswap(v[0], v[3]); cswap(v[5], v[8]); cswap(v[4], v[7]);
+    cswap(v[3], v[6]); cswap(v[1], v[4]); cswap(v[2], v[5]);
+    cswap(v[4], v[7]); cswap(v[4], v[2]); cswap(v[6], v[4]);
+    cswap(v[4], v[2]);
+    const unsigned char m = (unsigned char)v[4];
+    out[(long long)y * W + x] = make_uchar4(m, m, m, 255);
+}
+
+inline int finish() {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_hip_error(e);
+        return ASW_E_HIP;
+    }
+    return ASW_OK;
+}
+
+inline int d_end_of(const asw_params *p) { return p->d_end < 0 ? p->ndisp : p->d_end; }
+
+}  // namespace
+
+int launch_wta_scan(const asw_params *p, int mode, const float *cost, const float *ref_l, const float *ref_r,
+                    int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar, uint8_t *code_ref,
+                    uint8_t *code_tar, hipStream_t st) {
+    const long long S = (long long)p->width * p->height;
+    const int nwaves = (int)((S + 63) / 64);
+    const int per_xcd = (nwaves / 4 + 7) / 8 + 1;
+    const unsigned nblocks = 8u * (unsigned)per_xcd;
+    const int Dp = asw_disp_pitch(p);
+    if (mode == 0)
+        hipLaunchKernelGGL(k_wta_scan<0>, dim3(nblocks), dim3(256), 0, st, cost, p->width, p->height, Dp, p->ndisp,
+                           ref_l, ref_r, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, nwaves);
+    else
+        hipLaunchKernelGGL(k_wta_scan<1>, dim3(nblocks), dim3(256), 0, st, cost, p->width, p->height, Dp, p->ndisp,
+                           ref_l, ref_r, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, nwaves);
+    return finish();
+}
+
+}  // namespace asw
+
+using namespace asw;
+
+extern "C" {
+
+void asw_refine_params_default(asw_refine_params *rp) {
+    if (!rp) return;
+    rp->iters = 6;         // main.cpp:178 (k)
+    rp->taps = 33;         // K/asw_refinement_v.cl:33 (i < 33, y + i - 16)
+    rp->gamma_c = 10.94f;  // K/asw_refinement_v.cl:6
+    rp->gamma_g = 118.78f; // K/asw_refinement_v.cl:7
+    rp->alpha = 0.085f;    // K/asw_wta_ref.cl:28 (only the reference value is built)
+}
+
+int asw_refine_params_check(const asw_params *p, const asw_refine_params *rp) {
+    const int s = asw_params_check(p);
+    if (s != ASW_OK) return s;
+    if (!rp || rp->iters < 0 || rp->taps < 1 || (rp->taps & 1) == 0) return ASW_E_INVALID;
+    if (!(rp->gamma_c > 0.0f) || !(rp->gamma_g > 0.0f)) return ASW_E_INVALID;
+    if (rp->alpha != 0.085f) return ASW_E_UNSUPPORTED;
+    // the loop re-reads disparities through the reference's 8-bit codes
+    if (p->ndisp > 256 || p->lr_mode != ASW_LR_U8) return ASW_E_UNSUPPORTED;
+    if (p->d_begin != 0 || d_end_of(p) != p->ndisp) return ASW_E_UNSUPPORTED;  // whole volume on one device
+    return ASW_OK;
+}
+
+size_t asw_refine_lut_bytes(const asw_refine_params *rp) {
+    return rp ? (size_t)(rp->taps / 2 + 1) * kLutWidth * sizeof(float) : 0;
+}
+
+int asw_refine_lut(const asw_params *p, const asw_refine_params *rp, float *lut, void *stream) {
+    const int s = asw_refine_params_check(p, rp);
+    if (s != ASW_OK) return s;
+    asw_params q = *p;  // same table kernel, refinement falloffs and window
+    q.taps = rp->taps;
+    q.gamma_c = rp->gamma_c;
+    q.gamma_g = rp->gamma_g;
+    return asw_support_lut(&q, lut, stream);
+}
+
+int asw_wta_ref(const asw_params *p, const float *cost, const float *ref_l, const float *ref_r, int32_t *d_ref,
+                int32_t *d_tar, float *conf_ref, uint8_t *code_ref, uint8_t *code_tar, void *stream) {
+    const int s = asw_params_check(p);
+    if (s != ASW_OK) return s;
+    if (p->d_begin != 0 || d_end_of(p) != p->ndisp) return ASW_E_INVALID;
+    if (!cost || !ref_l || !ref_r || !d_ref || !d_tar || !conf_ref) return ASW_E_INVALID;
+    return launch_wta_scan(p, 1, cost, ref_l, ref_r, d_ref, conf_ref, d_tar, nullptr, code_ref, code_tar,
+                           (hipStream_t)stream);
+}
+
+int asw_ref_v(const asw_params *p, const asw_refine_params *rp, const uint8_t *img_rgba, const uint8_t *est,
+              int est_stride, const float *conf, const float *lut, float *out, void *stream) {
+    const int s = asw_refine_params_check(p, rp);
+    if (s != ASW_OK) return s;
+    if (!img_rgba || !est || !conf || !lut || !out || (est_stride != 1 && est_stride != 4)) return ASW_E_INVALID;
+    const dim3 grid((unsigned)((p->width + 255) / 256), (unsigned)p->height);
+    hipLaunchKernelGGL(k_ref_v, grid, dim3(256), 0, (hipStream_t)stream, reinterpret_cast<const uchar4 *>(img_rgba),
+                       est, est_stride, conf, lut, p->width, p->height, rp->taps, (float)(p->ndisp - 1), out);
+    return finish();
+}
+
+int asw_ref_h(const asw_params *p, const asw_refine_params *rp, const uint8_t *img_rgba, const float *conf,
+              const float *in, const float *lut, float *out, void *stream) {
+    const int s = asw_refine_params_check(p, rp);
+    if (s != ASW_OK) return s;
+    if (!img_rgba || !conf || !in || !lut || !out || in == out) return ASW_E_INVALID;
+    const dim3 grid((unsigned)((p->width + 255) / 256), (unsigned)p->height);
+    hipLaunchKernelGGL(k_ref_h, grid, dim3(256), 0, (hipStream_t)stream, reinterpret_cast<const uchar4 *>(img_rgba),
+                       conf, in, lut, p->width, p->height, rp->taps, out);
+    return finish();
+}
+
+int asw_median3(const asw_params *p, const uint8_t *codes, int stride, uint8_t *out_rgba, void *stream) {
+    const int s = asw_params_check(p);
+    if (s != ASW_OK) return s;
+    if (!codes || !out_rgba || (stride != 1 && stride != 4)) return ASW_E_INVALID;
+    const dim3 grid((unsigned)((p->width + 255) / 256), (unsigned)p->height);
+    hipLaunchKernelGGL(k_median3, grid, dim3(256), 0, (hipStream_t)stream, codes, stride, p->width, p->height,
+                       reinterpret_cast<uchar4 *>(out_rgba));
+    return finish();
+}
+
+size_t asw_refine_workspace_bytes(const asw_params *p, const asw_refine_params *rp) {
+    if (asw_refine_params_check(p, rp) != ASW_OK) return 0;
+    const size_t S = (size_t)p->width * p->height;
+    const size_t lut = (asw_refine_lut_bytes(rp) + 255) / 256 * 256;
+    // lut, 4 x [2][S] f32 (V/H estimates of both views), 2 x S int32, 2 x S u8 codes
+    return lut + 4 * 2 * S * 4 + 2 * S * 4 + 2 * S + 256;
+}
+
+int asw_refine(const asw_params *p, const asw_refine_params *rp, const uint8_t *left_rgba, const uint8_t *right_rgba,
+               const float *cost, uint8_t *est_left_rgba, uint8_t *code_tar, float *conf_ref, float *conf_tar,
+               void *workspace, uint8_t *post_red_rgba, uint8_t *final_rgba, int32_t *d_ref, int32_t *d_tar,
+               void *stream) {
+    int s = asw_refine_params_check(p, rp);
+    if (s != ASW_OK) return s;
+    if (!left_rgba || !right_rgba || !cost || !est_left_rgba || !code_tar || !conf_ref || !conf_tar || !workspace)
+        return ASW_E_INVALID;
+    const size_t S = (size_t)p->width * p->height;
+    char *ws = static_cast<char *>(workspace);
+    float *lut = reinterpret_cast<float *>(ws);
+    ws += (asw_refine_lut_bytes(rp) + 255) / 256 * 256;
+    float *vl = reinterpret_cast<float *>(ws), *vr = vl + 2 * S, *hl = vr + 2 * S, *hr = hl + 2 * S;
+    int32_t *dr = reinterpret_cast<int32_t *>(hr + 2 * S), *dt = dr + S;
+    uint8_t *kl = reinterpret_cast<uint8_t *>(dt + S);
+    hipStream_t st = (hipStream_t)stream;
+    if ((s = asw_refine_lut(p, rp, lut, st)) != ASW_OK) return s;
+    // main.cpp:541-612: the left estimate is channel 0 of consistency_error (RGBA),
+    // the right one the code image of the current target map
+    for (int it = 0; it < rp->iters; ++it) {
+        if ((s = asw_ref_v(p, rp, left_rgba, est_left_rgba, 4, conf_ref, lut, vl, st)) != ASW_OK) return s;
+        if ((s = asw_ref_v(p, rp, right_rgba, code_tar, 1, conf_tar, lut, vr, st)) != ASW_OK) return s;
+        if ((s = asw_ref_h(p, rp, left_rgba, conf_ref, vl, lut, hl, st)) != ASW_OK) return s;
+        if ((s = asw_ref_h(p, rp, right_rgba, conf_tar, vr, lut, hr, st)) != ASW_OK) return s;
+        if ((s = asw_wta_ref(p, cost, hl, hr, dr, dt, conf_ref, kl, code_tar, st)) != ASW_OK) return s;
+        if ((s = asw_consistency(p, dr, dt, kl, code_tar, conf_ref, conf_tar, est_left_rgba, post_red_rgba, st)) !=
+            ASW_OK)
+            return s;
+    }
+    if (final_rgba && (s = asw_median3(p, est_left_rgba, 4, final_rgba, st)) != ASW_OK) return s;
+    if (d_ref && rp->iters > 0 && hipMemcpyAsync(d_ref, dr, S * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return ASW_E_HIP;
+    if (d_tar && rp->iters > 0 && hipMemcpyAsync(d_tar, dt, S * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return ASW_E_HIP;
+    return ASW_OK;
+}
+
+}  // extern "C"

@@ -12,8 +12,10 @@
 //     634-708), here from HIP events (asw_timings);
 //   * outputs: <folder>/asw_consistency_pre-reff.png (the reference's file of the
 //     same name, main.cpp:625-627), asw_consistency.png (its `consistency_error`
-//     image) and asw_wta_disparity.png (its `asw_left_wta` image; the reference's
-//     asw_disparity.png is the post-refinement + median map, not produced here);
+//     image before refinement), asw_wta_disparity.png (its `asw_left_wta` image)
+//     and, with the k = 6 refinement iterations of main.cpp:540-617 (--refine K,
+//     0 = off), asw_disparity.png (refined + 3x3 median, main.cpp:619-623) and
+//     asw_consistency_post-reff.png (main.cpp:629-631);
 //   * errors are printed and the driver continues with the next pair, like ErCheck
 //     (main.cpp:27-30).
 #include <cstdio>
@@ -33,7 +35,7 @@ struct Options {
     std::string pics = "pics.txt";
     std::string root;  // default: directory of pics
     std::string tsv;   // default: "<device name>.tsv" in the current directory
-    int runs = 10, ndisp = 61, taps = 33, iters = 7, device = 0;
+    int runs = 10, ndisp = 61, taps = 33, iters = 7, device = 0, refine = 6;
     float gamma_c = -1.0f, gamma_g = -1.0f, tau = -1.0f;
     bool lab = false, lr = true, native_lr = false;
 };
@@ -42,7 +44,7 @@ void usage() {
     std::fprintf(stderr,
                  "usage: asw_stereo [--pics FILE] [--root DIR] [--runs N] [--ndisp D] [--taps T] [--iters R]\n"
                  "                  [--gamma-c G] [--gamma-g G] [--tau TAU] [--lab] [--no-lr] [--native-lr]\n"
-                 "                  [--device I] [--tsv FILE]\n");
+                 "                  [--refine K] [--device I] [--tsv FILE]\n");
 }
 
 bool parse(int argc, char **argv, Options &o) {
@@ -58,6 +60,7 @@ bool parse(int argc, char **argv, Options &o) {
         const char *v = nullptr;
         if (a == "--pics") { if (!(v = next("--pics"))) return false; o.pics = v; }
         else if (a == "--root") { if (!(v = next("--root"))) return false; o.root = v; }
+        else if (a == "--refine") { if (!(v = next("--refine"))) return false; o.refine = std::atoi(v); }
         else if (a == "--tsv") { if (!(v = next("--tsv"))) return false; o.tsv = v; }
         else if (a == "--runs") { if (!(v = next("--runs"))) return false; o.runs = std::atoi(v); }
         else if (a == "--ndisp") { if (!(v = next("--ndisp"))) return false; o.ndisp = std::atoi(v); }
@@ -156,17 +159,32 @@ int main(int argc, char **argv) {
             ++failures;
             continue;
         }
+        const bool refine = o.refine > 0 && p.lr_check;
+        if (refine) {
+            asw_refine_params rp;
+            asw_refine_params_default(&rp);
+            rp.iters = o.refine;
+            st = asw_set_refine(ctx, &rp);
+            if (st != ASW_OK) {
+                std::fprintf(stderr, "%s: asw_set_refine: %s\n", folder.c_str(), asw_strerror(st));
+                ++failures;
+                asw_destroy(ctx);
+                continue;
+            }
+        }
         const size_t S = (size_t)p.width * p.height;
-        std::vector<uint8_t> disp(S * 4), lr(S * 4), lr_red(S * 4);
+        std::vector<uint8_t> disp(S * 4), lr(S * 4), lr_red(S * 4), fin(S * 4), post(S * 4);
         asw_outputs out;
         std::memset(&out, 0, sizeof out);
         out.disp_rgba = disp.data();
         out.lr_rgba = lr.data();
         out.lr_red_rgba = lr_red.data();
+        out.final_rgba = refine ? fin.data() : nullptr;
+        out.post_red_rgba = refine ? post.data() : nullptr;
         if (tsv) {
             std::fprintf(tsv, "\n%s - %s\n", devname, folder.c_str());
             std::fprintf(tsv, "id\taggr\tsupp_w\tv_aggr_mean\th_aggr_mean\ttotal aggregation\twta\tconsistency\t"
-                              "total\th2d\td2h\n");
+                              "total\trefine\th2d\td2h\n");
         }
         for (int run = 0; run < o.runs && st == ASW_OK; ++run) {
             asw_timings t;
@@ -176,9 +194,9 @@ int main(int argc, char **argv) {
             std::printf("run %d: total %.3f ms (aggregation %.3f, V %.3f, H %.3f per pass)\n", run, t.total,
                         t.aggregation_total, t.v_pass_mean, t.h_pass_mean);
             if (tsv)
-                std::fprintf(tsv, "%d\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\n", run,
-                             t.raw_cost, t.support, t.v_pass_mean, t.h_pass_mean, t.aggregation_total, t.wta,
-                             t.consistency, t.total, t.h2d, t.d2h);
+                std::fprintf(tsv, "%d\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\n",
+                             run, t.raw_cost, t.support, t.v_pass_mean, t.h_pass_mean, t.aggregation_total, t.wta,
+                             t.consistency, t.total, t.refine, t.h2d, t.d2h);
         }
         asw_destroy(ctx);
         if (st != ASW_OK) {
@@ -193,9 +211,12 @@ int main(int argc, char **argv) {
             const std::vector<uint8_t> *img;
         } outs[] = {{"asw_wta_disparity.png", &disp},
                     {"asw_consistency.png", &lr},
-                    {"asw_consistency_pre-reff.png", &lr_red}};
+                    {"asw_consistency_pre-reff.png", &lr_red},
+                    {"asw_disparity.png", &fin},
+                    {"asw_consistency_post-reff.png", &post}};
         for (const auto &w : outs) {
             if (!p.lr_check && w.img != &disp) continue;
+            if (!refine && (w.img == &fin || w.img == &post)) continue;
             e = asw_host::png_save(dir + "/" + w.name, w.img->data(), L.width, L.height, 4);
             if (!e.empty()) {
                 std::fprintf(stderr, "%s: %s\n", folder.c_str(), e.c_str());

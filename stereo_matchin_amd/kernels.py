@@ -248,3 +248,88 @@ def wta_finalize(p: AswParams, key, m2, tkey, t2):
                                            _ptr(conf_ref), _ptr(d_tar), _ptr(conf_tar), _ptr(code_ref),
                                            _ptr(code_tar), _stream(dev)), "asw_wta_finalize")
     return d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar
+
+
+# --------------------------------------------------------------------------- refinement
+# main.cpp:540-623: k x (asw_ref_v, asw_ref_h on both views, asw_WTA_REF,
+# Constistency), then Median.  Estimates are [2][H][W] f32 (value plane, den plane).
+
+def refine_lut(p: AswParams, rp, device) -> torch.Tensor:
+    """Weight table of asw_ref_v / asw_ref_h (refinement falloffs 10.94 / 118.78)."""
+    lut = torch.empty((rp.taps // 2 + 1, 766), dtype=torch.float32, device=device)
+    _lib.check(_lib.lib().asw_refine_lut(ctypes.byref(p), ctypes.byref(rp), _ptr(lut), _stream(device)),
+               "asw_refine_lut")
+    return lut
+
+
+def asw_ref_v(p: AswParams, rp, img: torch.Tensor, est: torch.Tensor, conf: torch.Tensor, lut: torch.Tensor,
+              out: torch.Tensor | None = None):
+    """Vertical refinement (K/asw_refinement_v.cl:13-51).  ``est``: u8 codes [H][W]
+    or an RGBA8 image [H][W][4] (channel 0 is read, like read_imagef(...).x)."""
+    H, W = p.height, p.width
+    stride = 4 if est.dim() == 3 else 1
+    _expect(est, (H, W, 4) if stride == 4 else (H, W), torch.uint8, "est")
+    _expect(conf, (H, W), torch.float32, "conf")
+    if out is None:
+        out = torch.empty((2, H, W), dtype=torch.float32, device=img.device)
+    _expect(out, (2, H, W), torch.float32, "out")
+    _lib.check(_lib.lib().asw_ref_v(ctypes.byref(p), ctypes.byref(rp), _ptr(img), _ptr(est), stride, _ptr(conf),
+                                    _ptr(lut), _ptr(out), _stream(img.device)), "asw_ref_v")
+    return out
+
+
+def asw_ref_h(p: AswParams, rp, img: torch.Tensor, conf: torch.Tensor, est_v: torch.Tensor, lut: torch.Tensor,
+              out: torch.Tensor | None = None):
+    """Horizontal refinement (K/asw_refinement_h.cl:16-53) of asw_ref_v's output."""
+    H, W = p.height, p.width
+    _expect(est_v, (2, H, W), torch.float32, "est_v")
+    if out is None:
+        out = torch.empty_like(est_v)
+    _lib.check(_lib.lib().asw_ref_h(ctypes.byref(p), ctypes.byref(rp), _ptr(img), _ptr(conf), _ptr(est_v),
+                                    _ptr(lut), _ptr(out), _stream(img.device)), "asw_ref_h")
+    return out
+
+
+def asw_WTA_REF(p: AswParams, cost: torch.Tensor, ref_l: torch.Tensor, ref_r: torch.Tensor, conf_ref: torch.Tensor):
+    """Penalised WTA (K/asw_wta_ref.cl:2-68).  Writes the TARGET confidence into
+    ``conf_ref`` (the reference's second store to ``confidence``); returns
+    ``(d_ref, d_tar, code_ref, code_tar)``."""
+    _expect(cost, cost_shape(p), torch.float32, "cost")
+    H, W = p.height, p.width
+    dev = cost.device
+    d_ref = torch.empty((H, W), dtype=torch.int32, device=dev)
+    d_tar = torch.empty_like(d_ref)
+    code_ref = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    code_tar = torch.empty_like(code_ref)
+    _lib.check(_lib.lib().asw_wta_ref(ctypes.byref(p), _ptr(cost), _ptr(ref_l), _ptr(ref_r), _ptr(d_ref),
+                                      _ptr(d_tar), _ptr(conf_ref), _ptr(code_ref), _ptr(code_tar), _stream(dev)),
+               "asw_wta_ref")
+    return d_ref, d_tar, code_ref, code_tar
+
+
+def Median(p: AswParams, codes: torch.Tensor) -> torch.Tensor:
+    """3x3 median (K/median.cl:58-88) of u8 codes [H][W] or of channel 0 of RGBA8 [H][W][4]."""
+    stride = 4 if codes.dim() == 3 else 1
+    out = torch.empty((p.height, p.width, 4), dtype=torch.uint8, device=codes.device)
+    _lib.check(_lib.lib().asw_median3(ctypes.byref(p), _ptr(codes), stride, _ptr(out), _stream(codes.device)),
+               "asw_median3")
+    return out
+
+
+def refine(p: AswParams, rp, left, right, cost, est_left_rgba, code_tar, conf_ref, conf_tar) -> dict:
+    """The whole loop (asw_refine).  est_left_rgba, code_tar, conf_ref, conf_tar are
+    updated in place like the reference's buffers; returns the outputs."""
+    H, W = p.height, p.width
+    dev = cost.device
+    ws = torch.empty(int(_lib.lib().asw_refine_workspace_bytes(ctypes.byref(p), ctypes.byref(rp))),
+                     dtype=torch.uint8, device=dev)
+    if ws.numel() == 0:
+        _lib.check(_lib.lib().asw_refine_params_check(ctypes.byref(p), ctypes.byref(rp)), "asw_refine_params_check")
+    post = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+    final = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
+    d_ref = torch.empty((H, W), dtype=torch.int32, device=dev)
+    d_tar = torch.empty_like(d_ref)
+    _lib.check(_lib.lib().asw_refine(ctypes.byref(p), ctypes.byref(rp), _ptr(left), _ptr(right), _ptr(cost),
+                                     _ptr(est_left_rgba), _ptr(code_tar), _ptr(conf_ref), _ptr(conf_tar), _ptr(ws),
+                                     _ptr(post), _ptr(final), _ptr(d_ref), _ptr(d_tar), _stream(dev)), "asw_refine")
+    return {"post_red_rgba": post, "final_rgba": final, "d_ref": d_ref, "d_tar": d_tar}

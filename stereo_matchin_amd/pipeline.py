@@ -116,6 +116,16 @@ class StereoMatcher:
             events.append(("consistency", _record()))
         return MatchResult(d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, lr, red, cost)
 
+    def refine(self, res: MatchResult, left: torch.Tensor, right: torch.Tensor, rp=None) -> dict:
+        """The refinement loop + median (main.cpp:540-623) after ``match`` (needs its LR
+        check).  ``res``'s lr image, target codes and confidences are refined in place
+        like the reference's buffers; returns post_red_rgba (asw_consistency_post-reff),
+        final_rgba (asw_disparity.png) and the last asw_WTA_REF maps."""
+        if res.lr_rgba is None:
+            raise ValueError("refinement starts from the consistency image: match() with lr_check")
+        rp = _lib.default_refine_params() if rp is None else rp
+        return K.refine(self.p, rp, left, right, res.cost, res.lr_rgba, res.code_tar, res.conf_ref, res.conf_tar)
+
 
 def _record():
     e = torch.cuda.Event(enable_timing=True)
@@ -135,7 +145,7 @@ def to_rgba(img: np.ndarray) -> np.ndarray:
 
 
 def match_frame(params: AswParams, left_rgba: np.ndarray, right_rgba: np.ndarray, device: int = 0,
-                want_cost: bool = False) -> dict:
+                want_cost: bool = False, refine=None) -> dict:
     """Frame API (``asw_create`` + ``asw_match``): host RGBA8 in, host maps out."""
     L = _lib.lib()
     H, W = params.height, params.width
@@ -153,9 +163,13 @@ def match_frame(params: AswParams, left_rgba: np.ndarray, right_rgba: np.ndarray
         }
         if want_cost:
             out["cost"] = np.empty((H, W, _lib.disp_pitch(params)), np.float32)
+        if refine is not None:  # an AswRefineParams: main.cpp:540-623 inside asw_match
+            _lib.check(L.asw_set_refine(ctx, ctypes.byref(refine)), "asw_set_refine")
+            out["final_rgba"] = np.empty((H, W, 4), np.uint8)
+            out["post_red_rgba"] = np.empty((H, W, 4), np.uint8)
         o = _lib.AswOutputs(*[out[k].ctypes.data if k in out else None for k in
                               ("d_ref", "d_tar", "conf_ref", "conf_tar", "disp_rgba", "lr_rgba", "lr_red_rgba",
-                               "cost")])
+                               "cost", "final_rgba", "post_red_rgba")])
         t = _lib.AswTimings()
         _lib.check(L.asw_match(ctx, left_rgba.ctypes.data, right_rgba.ctypes.data, ctypes.byref(o), ctypes.byref(t)),
                    "asw_match")
