@@ -160,7 +160,7 @@ def test_den_cache_write_then_read(gpu, oracle, T, direction, H, W, D, d0, d1):
 
 # every compiled pass variant (asw_tune_set): block shapes, 8-wave V, and the
 # diagonal-pair H kernel (Dp % 128 == 0), on shapes that hit segment / row edges
-@pytest.mark.parametrize("variant", [0, 2, 4, 8, 16])
+@pytest.mark.parametrize("variant", [0, 8, 64, 128, 32, 34, 36, 40, 48])
 @pytest.mark.parametrize("H,W,D,d0,d1", [(9, 331, 256, 0, 256), (6, 47, 128, 0, 128), (5, 161, 300, 40, 168),
                                           (4, 400, 256, 128, 256)])
 def test_pass_variants_bit_exact(gpu, oracle, variant, H, W, D, d0, d1):

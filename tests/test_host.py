@@ -184,5 +184,7 @@ def test_cli_tsukuba_reproduces_reference_png(tmp_path):
     np.testing.assert_array_equal(out, dev_red)
     for name in ("asw_wta_disparity.png", "asw_consistency.png"):
         assert (d / name).exists()
-    rows = [ln for ln in tsv.read_text().splitlines() if ln[:1].isdigit()]
-    assert len(rows) == 2 and all(len(ln.split("\t")) == 11 for ln in rows)
+    lines = tsv.read_text().splitlines()
+    header = next(ln for ln in lines if ln.startswith("id\t"))
+    rows = [ln for ln in lines if ln[:1].isdigit()]
+    assert len(rows) == 2 and all(len(ln.split("\t")) == len(header.split("\t")) for ln in rows)
