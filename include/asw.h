@@ -126,6 +126,14 @@ int asw_aggregate_pass(const asw_params *p, int dir, const float *wl, const floa
 int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin,
                            float *cout, float *den, int den_mode, void *stream);
 
+/* The first V pass of main.cpp:494-500 with asw_Aggr (main.cpp:463-466,
+ * K/asw_aggr.cl:3-23) fused: each window element's raw AD/TAD cost is computed
+ * from the two RGBA8 images (device pointers) instead of read from a raw-cost
+ * volume, so that volume is never written nor read.  cout (and den per den_mode)
+ * are bit-identical to asw_raw_cost followed by asw_aggregate_pass_den(V). */
+int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
+                           const uint8_t *right_rgba, float *cout, float *den, int den_mode, void *stream);
+
 /* r x (V,H) ping-pong of main.cpp:486-515 on two caller buffers; the result
  * ends in `c0` (c0 holds the raw cost on entry, c1 is scratch). */
 int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,

@@ -11,13 +11,13 @@ namespace agg {
 int g_pass_variant = 0;
 template <int T, int DM>
 int launch_pass_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                   float *den, hipStream_t st);
+                   float *den, hipStream_t st, const RawSrc *raw);
 template <int T>
 int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                  float *den, int dm, hipStream_t st) {
-    if (dm == 1) return launch_pass_tm<T, 1>(p, dir, wl, wr, cin, cout, den, st);
-    if (dm == 2) return launch_pass_tm<T, 2>(p, dir, wl, wr, cin, cout, den, st);
-    return launch_pass_tm<T, 0>(p, dir, wl, wr, cin, cout, den, st);
+                  float *den, int dm, hipStream_t st, const RawSrc *raw) {
+    if (dm == 1) return launch_pass_tm<T, 1>(p, dir, wl, wr, cin, cout, den, st, raw);
+    if (dm == 2) return launch_pass_tm<T, 2>(p, dir, wl, wr, cin, cout, den, st, raw);
+    return launch_pass_tm<T, 0>(p, dir, wl, wr, cin, cout, den, st, raw);
 }
 }  // namespace agg
 
@@ -28,12 +28,12 @@ int set_pass_variant(int v) {
 }
 
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                float *den, int dm, hipStream_t st) {
+                float *den, int dm, hipStream_t st, const RawSrc *raw) {
     if (dm != 0 && !den) return ASW_E_INVALID;
     switch (p->taps) {
 #define ASW_CASE(TT) \
     case TT:         \
-        return agg::launch_pass_t<TT>(p, dir, wl, wr, cin, cout, den, dm, st);
+        return agg::launch_pass_t<TT>(p, dir, wl, wr, cin, cout, den, dm, st, raw);
         ASW_CASE(3)
         ASW_CASE(5)
         ASW_CASE(7)

@@ -31,10 +31,18 @@ __host__ __device__ inline int code_u8(int d, int D) {
 
 void set_hip_error(hipError_t e);
 
+// last plane + 1 of the context's disparity shard (asw_params.d_end < 0: ndisp)
+__host__ __device__ inline int d_end_of_p(const asw_params *p) { return p->d_end < 0 ? p->ndisp : p->d_end; }
+
+// images of a V pass with the raw cost fused (asw_aggregate_pass_raw)
+struct RawSrc {
+    const uint8_t *left, *right;
+};
+
 // one aggregation pass over every local plane (asw_aggregate.hip)
 // den/dm: cached-denominator mode (ASW_DEN_*; den = NULL with ASW_DEN_NONE)
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                float *den, int dm, hipStream_t st);
+                float *den, int dm, hipStream_t st, const RawSrc *raw = nullptr);
 int set_pass_variant(int v);
 
 // lane-per-pixel WTA scan (asw_refine.hip): mode 0 = asw_WTA, 1 = asw_WTA_REF

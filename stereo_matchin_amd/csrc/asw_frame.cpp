@@ -204,7 +204,10 @@ int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
     HIPCHK(hipMemcpyAsync(c->left, left_rgba, S * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(c->right, right_rgba, S * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(ev[1], st));
-    ASWCHK(asw_raw_cost(p, c->left, c->right, c->c0, st));
+    // asw_Aggr is fused into the first V pass (asw_aggregate_pass_raw): the raw
+    // cost volume is never materialised and the "aggr" time slot stays empty,
+    // unless there is no pass at all (r = 0)
+    if (r == 0) ASWCHK(asw_raw_cost(p, c->left, c->right, c->c0, st));
     HIPCHK(hipEventRecord(ev[2], st));
     if (p->color_space == ASW_COLOR_LAB) {
         ASWCHK(asw_lab(p, c->left, c->lab_l, st));
@@ -224,7 +227,10 @@ int asw_match(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
     if (timed) HIPCHK(hipEventRecord(ev[e_pass0], st));
     for (int it = 0; it < r; ++it) {
         const int dm = !c->den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
-        ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, c->wvl, c->wvr, c->c0, c->c1, c->den_v, dm, st));
+        if (it == 0)
+            ASWCHK(asw_aggregate_pass_raw(p, c->wvl, c->wvr, c->left, c->right, c->c1, c->den_v, dm, st));
+        else
+            ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, c->wvl, c->wvr, c->c0, c->c1, c->den_v, dm, st));
         if (timed) HIPCHK(hipEventRecord(ev[e_pass0 + 2 * it + 1], st));
         ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, c->whl, c->whr, c->c1, c->c0, c->den_h, dm, st));
         if (timed) HIPCHK(hipEventRecord(ev[e_pass0 + 2 * it + 2], st));

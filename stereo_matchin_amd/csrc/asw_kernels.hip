@@ -578,6 +578,16 @@ int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const 
     return asw::launch_pass(p, dir, wl, wr, cin, cout, den, den_mode, (hipStream_t)stream);
 }
 
+int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
+                           const uint8_t *right_rgba, float *cout, float *den, int den_mode, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!wvl || !wvr || !left_rgba || !right_rgba || !cout) return ASW_E_INVALID;
+    if (den_mode < ASW_DEN_NONE || den_mode > ASW_DEN_READ) return ASW_E_INVALID;
+    if (den_mode != ASW_DEN_NONE && (!den || den == cout)) return ASW_E_INVALID;
+    const asw::RawSrc raw{left_rgba, right_rgba};
+    return asw::launch_pass(p, ASW_DIR_V, wvl, wvr, nullptr, cout, den, den_mode, (hipStream_t)stream, &raw);
+}
+
 int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
                   float *c0, float *c1, void *stream) {
     return asw_aggregate_den(p, wvl, wvr, whl, whr, c0, c1, nullptr, nullptr, stream);

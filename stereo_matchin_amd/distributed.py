@@ -117,10 +117,11 @@ class ShardedStereoMatcher:
         m = self.matcher
         if events is not None:
             events.append(("start", _record()))
-        m.raw_and_support(left, right)
+        fuse = m.fuse_raw and self.p.iters >= 1  # asw_Aggr fused into the first V pass
+        m.raw_and_support(left, right, raw=not fuse)
         if events is not None:
             events.append(("support", _record()))
-        cost = m.aggregate(events)
+        cost = m.aggregate(events, images=(left, right) if fuse else None)
         d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = sharded_wta(self.ops, cost, self.reduce_min)
         if events is not None:
             events.append(("wta", _record()))

@@ -162,6 +162,26 @@ def asw_vCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None,
     return _pass(p, DIR_V, supp_left, supp_right, cost_in, out, den, den_mode)
 
 
+def asw_vCostAggregation_raw(p: AswParams, supp_left, supp_right, left, right, out=None, den=None,
+                             den_mode: int = 0):
+    """The first vertical pass with asw_Aggr fused (K/asw_aggr.cl:3-23 then
+    K/asw_vcost_aggregation.cl:11-44): the window's raw costs come from the images,
+    no raw-cost volume.  Same result as ``asw_vCostAggregation(asw_Aggr(...))``."""
+    _expect(supp_left, support_shape(p), torch.float32, "supp_left")
+    _expect(supp_right, support_shape(p), torch.float32, "supp_right")
+    _expect(left, (p.height, p.width, 4), torch.uint8, "left")
+    _expect(right, (p.height, p.width, 4), torch.uint8, "right")
+    if out is None:
+        out = new_cost(p, left.device)
+    _expect(out, cost_shape(p), torch.float32, "out")
+    if den_mode:
+        _expect(den, cost_shape(p), torch.float32, "den")
+    _lib.check(_lib.lib().asw_aggregate_pass_raw(ctypes.byref(p), _ptr(supp_left), _ptr(supp_right), _ptr(left),
+                                                 _ptr(right), _ptr(out), _ptr(den), den_mode, _stream(left.device)),
+               "asw_aggregate_pass_raw")
+    return out
+
+
 def asw_hCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None, den=None, den_mode: int = 0):
     """One horizontal weighted-aggregation pass (K/asw_hcost_aggregation.cl:12-44)."""
     return _pass(p, DIR_H, supp_left, supp_right, cost_in, out, den, den_mode)

@@ -48,11 +48,14 @@ class StereoMatcher:
     (V, H) as volumes — written by the first pass of each direction, read by the
     other r-1 (ASW_DEN_*); bit-identical results, 2 more cost-sized buffers."""
 
-    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True):
+    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool = False):
         st = _lib.params_check(params)
         if st != _lib.ASW_OK:
             raise _lib.AswError(st, "asw_params_check")
         self.p = params.copy()
+        # asw_Aggr fused into the first V pass: bit-identical, but measured slower on
+        # MI355X (3.10 ms vs 2.02 + 0.64 ms, profiles/r01/kernel_stats_fused_raw.csv)
+        self.fuse_raw = fuse_raw
         self.device = torch.device(device)
         dev = self.device
         self.lut = torch.empty(K.lut_shape(self.p), dtype=torch.float32, device=dev)
@@ -68,9 +71,12 @@ class StereoMatcher:
             self.den_h = K.new_cost(self.p, dev)
 
     # -- stages ---------------------------------------------------------------
-    def raw_and_support(self, left: torch.Tensor, right: torch.Tensor):
+    def raw_and_support(self, left: torch.Tensor, right: torch.Tensor, raw: bool = True):
+        """asw_Aggr into c0 (unless ``raw`` is False: the first V pass computes it,
+        see ``aggregate(images=...)``) and the four support arrays."""
         p = self.p
-        K.asw_Aggr(p, left, right, out=self.c0)
+        if raw:
+            K.asw_Aggr(p, left, right, out=self.c0)
         if p.color_space == COLOR_LAB:
             lab_l, lab_r = K.lab_image(p, left), K.lab_image(p, right)
             K.support_lab(p, DIR_V, lab_l, out=self.wvl)
@@ -84,12 +90,18 @@ class StereoMatcher:
         K.asw_vSupport(p, right, self.lut, out=self.wvr)
         K.asw_hSupport(p, right, self.lut, out=self.whr)
 
-    def aggregate(self, events: list | None = None):
-        """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515)."""
+    def aggregate(self, events: list | None = None, images: tuple | None = None):
+        """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515).
+        ``images`` = (left, right): the first V pass computes the raw cost itself
+        (asw_aggregate_pass_raw) and c0's input content is not used."""
         p = self.p
         for it in range(p.iters):
             dm = _lib.DEN_NONE if self.den_v is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
-            K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1, den=self.den_v, den_mode=dm)
+            if it == 0 and images is not None:
+                K.asw_vCostAggregation_raw(p, self.wvl, self.wvr, images[0], images[1], out=self.c1, den=self.den_v,
+                                           den_mode=dm)
+            else:
+                K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1, den=self.den_v, den_mode=dm)
             if events is not None:
                 events.append(("v", _record()))
             K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0, den=self.den_h, den_mode=dm)
@@ -102,10 +114,11 @@ class StereoMatcher:
         p = self.p
         if events is not None:
             events.append(("start", _record()))
-        self.raw_and_support(left, right)
+        fuse = self.fuse_raw and p.iters >= 1  # asw_Aggr fused into the first V pass
+        self.raw_and_support(left, right, raw=not fuse)
         if events is not None:
             events.append(("support", _record()))
-        cost = self.aggregate(events)
+        cost = self.aggregate(events, images=(left, right) if fuse else None)
         d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.asw_WTA(p, cost)
         if events is not None:
             events.append(("wta", _record()))

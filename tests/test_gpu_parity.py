@@ -158,6 +158,40 @@ def test_den_cache_write_then_read(gpu, oracle, T, direction, H, W, D, d0, d1):
         assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
 
 
+# asw_Aggr fused into the first V pass (asw_aggregate_pass_raw): bit-identical to
+# asw_raw_cost + asw_aggregate_pass_den(V), incl. a d-shard, padding planes (D not a
+# multiple of 64), truncated AD, every den mode, and the den volume it writes
+@pytest.mark.parametrize("T", [5, 9, 33, 35, 51])
+@pytest.mark.parametrize("H,W,D,d0,d1,tau", [(37, 91, 70, 0, 70, 765.0), (23, 150, 200, 70, 135, 765.0),
+                                              (40, 77, 64, 0, 64, 90.0), (3, 5, 9, 0, 9, 765.0)])
+def test_raw_fused_first_v_pass(gpu, oracle, T, H, W, D, d0, d1, tau):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    Lh, Rh = _rand_pair(T * 7 + W + D, H, W, shift=6)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1, tad_tau=tau)
+    L, R = _t(Lh, gpu), _t(Rh, gpu)
+    wl, wr = K.asw_vSupport(p, L), K.asw_vSupport(p, R)
+    c0 = K.asw_Aggr(p, L, R)
+    for mode in (_lib.DEN_NONE, _lib.DEN_WRITE):
+        den_a = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+        den_b = den_a.clone()
+        want = K.asw_vCostAggregation(p, wl, wr, c0, den=den_a, den_mode=mode)
+        got = K.asw_vCostAggregation_raw(p, wl, wr, L, R, den=den_b, den_mode=mode)
+        n = d1 - d0
+        assert torch.equal(got[..., :n], want[..., :n]), (mode, torch.nonzero(got[..., :n] != want[..., :n])[:5])
+        if mode == _lib.DEN_WRITE:
+            assert torch.equal(den_b[..., :n], den_a[..., :n])
+    # and against the oracle's raw cost + pass
+    full = oracle.raw_cost_tad(Lh, Rh, D, tau) if tau < 765 else oracle.raw_cost(Lh, Rh, D)
+    cin = np.ascontiguousarray(full[d0:d1])
+    sl, sr = oracle.support(Lh, T, 0), oracle.support(Rh, T, 0)
+    want = oracle.aggregate_pass(sl, sr, cin, T, 0, d0=d0, d1=d1, plane_base=d0)
+    got = plane_major(_np(K.asw_vCostAggregation_raw(p, wl, wr, L, R)), d1 - d0)
+    assert np.array_equal(got, want)
+
+
 # every compiled pass variant (asw_tune_set): block shapes, 8-wave V, and the
 # diagonal-pair H kernel (Dp % 128 == 0), on shapes that hit segment / row edges
 @pytest.mark.parametrize("variant", [0, 8, 64, 128, 32, 34, 36, 40, 48])
@@ -205,10 +239,10 @@ def test_wta_and_consistency_on_oracle_volume(gpu, oracle):
 
 # ------------------------------------------------------------------ end to end
 
-def _run(gpu, Lh, Rh, D, T, iters, **kw):
+def _run(gpu, Lh, Rh, D, T, iters, fuse_raw=False, **kw):
     from stereo_matchin_amd import StereoMatcher
     p = _params(Lh.shape[1], Lh.shape[0], D, T, iters, **kw)
-    m = StereoMatcher(p, gpu)
+    m = StereoMatcher(p, gpu, fuse_raw=fuse_raw)
     return p, m.match(_t(Lh, gpu), _t(Rh, gpu))
 
 
@@ -234,9 +268,10 @@ def test_e2e_tsukuba_reference_params(gpu, oracle):
     assert np.array_equal(_np(res.lr_red_rgba)[..., :3], dev_red)
 
 
-def test_e2e_c1_tsukuba_d16_t5(gpu, oracle):
+@pytest.mark.parametrize("fuse_raw", [False, True])
+def test_e2e_c1_tsukuba_d16_t5(gpu, oracle, fuse_raw):
     Lh, Rh, _ = load_scene("tsukuba")
-    _, res = _run(gpu, Lh, Rh, 16, 5, 7)
+    _, res = _run(gpu, Lh, Rh, 16, 5, 7, fuse_raw=fuse_raw)
     _compare_e2e(res, oracle.match(Lh, Rh, 16, 5, 7, want_cost=True), 16)
 
 
