@@ -136,7 +136,25 @@ __global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost
     const float *crow = cost + (long long)y * W * Dp;
     float cur_t = kSentinel, last_t = kSentinel;
     int mdr = md;
-    for (int i = 0; i < md; ++i) {
+    // the diagonal gathers are independent of the scan: issue 8 before consuming
+    // any, so the loop is bound by load throughput rather than one latency per plane
+    int i = 0;
+    for (; i + 8 <= md; i += 8) {
+        float tv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int xq = x - (i + k) < 0 ? 0 : x - (i + k);
+            tv[k] = crow[(long long)xq * Dp + (md + xq - x)];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int xq = x - (i + k) < 0 ? 0 : x - (i + k);
+            float t = tv[k];
+            if constexpr (MODE == 1) t = penalty(at, valt, i + k, t);
+            scan_step(t, md + xq - x, cur_t, last_t, mdr);
+        }
+    }
+    for (; i < md; ++i) {
         const int xq = x - i < 0 ? 0 : x - i;
         const int b = md + xq - x;
         float t = crow[(long long)xq * Dp + b];
