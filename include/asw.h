@@ -38,6 +38,7 @@ extern "C" {
 #define ASW_E_HIP -2         /* a HIP runtime call failed (asw_last_hip_error) */
 #define ASW_E_NOMEM -3       /* device or host allocation failed              */
 #define ASW_E_UNSUPPORTED -4 /* parameter combination not built               */
+#define ASW_E_COMM -5        /* a collective (RCCL) call failed               */
 
 #define ASW_DIR_V 0 /* vertical pass / support   (asw_vSupport, asw_vCostAggregation) */
 #define ASW_DIR_H 1 /* horizontal pass / support (asw_hSupport, asw_hCostAggregation) */
@@ -243,26 +244,71 @@ typedef struct asw_outputs { /* caller-owned host arrays; any may be NULL */
     float *cost;             /* [H][W][Dp] final aggregated volume (optional)   */
     uint8_t *final_rgba;     /* [H][W][4] asw_disparity.png (refinement on)     */
     uint8_t *post_red_rgba;  /* [H][W][4] asw_consistency_post-reff.png (refinement on) */
+    /* 16-bit disparity images: the 8-bit codes of K/asw_wta.cl:70-74
+     * collide above D = 256 (C5: D = 512); these hold the disparity index itself. */
+    uint16_t *disp16;        /* [H][W] d_ref                                              */
+    uint16_t *lr16;          /* [H][W] d_ref where the LR check passes, else ASW_DISP16_INVALID
+                                (the asw_consistency_pre-reff image; lr_check only)        */
 } asw_outputs;
+#define ASW_DISP16_INVALID 0xFFFF
 
 typedef struct asw_timings { /* milliseconds from HIP events, columns of main.cpp:181 */
     double raw_cost, support, v_pass_mean, h_pass_mean, aggregation_total, wta, consistency, total;
     double h2d, d2h;
     double refine;           /* refinement loop + median (0 when off) */
+    double exchange;         /* multi-GPU contexts: the WTA exchange (4 MIN all-reduces) */
 } asw_timings;
 
 /* marketing name of a HIP device (the reference names its TSV after the OpenCL
  * device, main.cpp:164-166); writes a NUL-terminated string of at most len bytes. */
 int asw_device_name(int hip_device, char *buf, int len);
 
-/* one context = one GPU (HIP device ordinal) and one disparity shard. */
+/* A context owns the device buffers of one image size, sized at create and reused
+ * by every asw_match (the reference re-creates its cl_mem objects per run,
+ * main.cpp:243-457).  p->d_begin / d_end must cover the whole range: contexts
+ * shard the disparity axis themselves.
+ *
+ * asw_create: one GPU (HIP device ordinal), the whole disparity range. */
 int asw_create(const asw_params *p, int hip_device, asw_ctx **out);
+/* One process, n_devices GPUs: [0, ndisp) is split into n_devices
+ * contiguous shards, shard i on hip_device_ids[i].  Raw cost, supports and the 2r
+ * passes of a shard touch only its planes (no communication); the WTA is the one
+ * exchange: 4 elementwise MIN all-reduces of S-element arrays (int64 keys
+ * (float_bits(m1) << 32 | d) and float second minima, the asw_wta_local protocol).
+ * They run over RCCL (ncclAllReduce / ncclMin in one ncclGroupStart/End, one
+ * communicator per device from ncclCommInitAll) when the ids are distinct, and as
+ * peer copies + a MIN kernel on hip_device_ids[0] when an id repeats (several
+ * shards on one GPU).  The LR check and every output are on hip_device_ids[0];
+ * results equal a one-GPU context bit for bit. */
+int asw_create_multi(const asw_params *p, const int *hip_device_ids, int n_devices, asw_ctx **out);
+/* Multi-process (one process per GPU): this process is shard `rank` of `nranks`,
+ * the all-reduces run over an RCCL communicator made from `id` (ncclCommInitRank);
+ * asw_comm_unique_id makes the id on one rank (ncclGetUniqueId) and the caller
+ * shares it with the others (MPI, torch.distributed, a file).  Every rank returns
+ * the whole frame's outputs. */
+#define ASW_COMM_ID_BYTES 128
+int asw_comm_unique_id(uint8_t id[ASW_COMM_ID_BYTES]);
+int asw_create_rank(const asw_params *p, int hip_device, int rank, int nranks, const uint8_t id[ASW_COMM_ID_BYTES],
+                    asw_ctx **out);
+/* shard layout of a context: number of shards it drives in this process and the
+ * [d_begin, d_end) of shard i (ASW_E_INVALID for i out of range) */
+int asw_ctx_shard(const asw_ctx *ctx, int i, int *n_shards, int *d_begin, int *d_end);
 int asw_destroy(asw_ctx *ctx);
+/* One stereo pair, host RGBA8 in, host outputs out (any output pointer may be NULL). */
 int asw_match(asw_ctx *ctx, const uint8_t *left_rgba, const uint8_t *right_rgba, asw_outputs *out,
               asw_timings *t);
+/* `batch` pairs (SURVEY §8(b) `asw_match(ctx, L, R, batch, ...)`): left_rgba /
+ * right_rgba hold `batch` consecutive [H][W][4] images, out[b] and t[b] (t may be
+ * NULL) receive pair b.  The pairs stream through the context's one set of
+ * volumes (a 3840x2160 D512 pair needs ~75 GB with cached denominators; 8 of them
+ * are never resident together). */
+int asw_match_batch(asw_ctx *ctx, const uint8_t *left_rgba, const uint8_t *right_rgba, int batch,
+                    asw_outputs *out, asw_timings *t);
 /* turn the refinement loop on for later asw_match calls (rp = NULL or iters = 0:
- * off, the default).  Needs lr_check; asw_match then fills final_rgba /
- * post_red_rgba and leaves lr_rgba as the pre-refinement consistency image. */
+ * off, the default).  Needs lr_check and a one-shard context.  asw_match then
+ * fills final_rgba / post_red_rgba; every other output (d_ref, d_tar, conf_*,
+ * disp_rgba, lr_rgba, lr_red_rgba, disp16, lr16) stays the pre-refinement result
+ * (they are copied out before the loop updates its buffers in place). */
 int asw_set_refine(asw_ctx *ctx, const asw_refine_params *rp);
 
 #ifdef __cplusplus

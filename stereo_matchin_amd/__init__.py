@@ -8,9 +8,11 @@ reference's kernel interface (:mod:`.kernels`), the one-GPU pipeline
 """
 from ._lib import (ASW_OK, COLOR_LAB, COLOR_RGB, DIR_H, DIR_V, LR_NATIVE, LR_U8, AswError,  # noqa: F401
                    AswLibraryError, AswParams, default_params)
-from .pipeline import MatchResult, StereoMatcher, make_params, match_frame, to_rgba  # noqa: F401
+from .pipeline import (FrameContext, MatchResult, StereoMatcher, comm_unique_id, make_params,  # noqa: F401
+                       match_frame, to_rgba)
 
 __all__ = [
     "AswParams", "AswError", "AswLibraryError", "StereoMatcher", "MatchResult", "make_params", "match_frame",
+    "FrameContext", "comm_unique_id",
     "to_rgba", "default_params",
 ]

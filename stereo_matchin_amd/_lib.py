@@ -28,6 +28,9 @@ ASW_E_INVALID = -1
 ASW_E_HIP = -2
 ASW_E_NOMEM = -3
 ASW_E_UNSUPPORTED = -4
+ASW_E_COMM = -5
+DISP16_INVALID = 0xFFFF
+COMM_ID_BYTES = 128
 
 DIR_V = 0
 DIR_H = 1
@@ -83,6 +86,7 @@ class AswOutputs(ctypes.Structure):
         ("disp_rgba", ctypes.c_void_p), ("lr_rgba", ctypes.c_void_p),
         ("lr_red_rgba", ctypes.c_void_p), ("cost", ctypes.c_void_p),
         ("final_rgba", ctypes.c_void_p), ("post_red_rgba", ctypes.c_void_p),
+        ("disp16", ctypes.c_void_p), ("lr16", ctypes.c_void_p),
     ]
 
 
@@ -96,7 +100,7 @@ class AswRefineParams(ctypes.Structure):
 class AswTimings(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in (
         "raw_cost", "support", "v_pass_mean", "h_pass_mean", "aggregation_total", "wta",
-        "consistency", "total", "h2d", "d2h", "refine")]
+        "consistency", "total", "h2d", "d2h", "refine", "exchange")]
 
 
 _lib = None
@@ -152,6 +156,11 @@ SIGNATURES = {
     "asw_create": (I, [PP, I, ctypes.POINTER(P)]),
     "asw_destroy": (I, [P]),
     "asw_match": (I, [P, P, P, ctypes.POINTER(AswOutputs), ctypes.POINTER(AswTimings)]),
+    "asw_create_multi": (I, [PP, ctypes.POINTER(I), I, ctypes.POINTER(P)]),
+    "asw_comm_unique_id": (I, [ctypes.c_char_p]),
+    "asw_create_rank": (I, [PP, I, I, I, ctypes.c_char_p, ctypes.POINTER(P)]),
+    "asw_ctx_shard": (I, [P, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(I)]),
+    "asw_match_batch": (I, [P, P, P, I, ctypes.POINTER(AswOutputs), ctypes.POINTER(AswTimings)]),
 }
 
 

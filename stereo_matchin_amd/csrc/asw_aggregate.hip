@@ -30,6 +30,15 @@ int set_pass_variant(int v) {
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                 float *den, int dm, hipStream_t st, const RawSrc *raw) {
     if (dm != 0 && !den) return ASW_E_INVALID;
+    // the pass kernels address the cost volume with 32-bit buffer offsets of up to
+    // ~2T+16 rows from a per-chunk base, and a support array from its base
+    const long long rowbytes = (long long)p->width * asw_disp_pitch(p) * 4;
+    if (rowbytes * (2LL * p->taps + 16) >= (1LL << 31)) return ASW_E_UNSUPPORTED;
+    if ((long long)asw_support_bytes(p) >= (1LL << 31)) return ASW_E_UNSUPPORTED;
+#ifdef ASW_DEV_TAPS  // development build (make DEV=1): one tap count only
+    if (p->taps != ASW_DEV_TAPS) return ASW_E_UNSUPPORTED;
+    return agg::launch_pass_t<ASW_DEV_TAPS>(p, dir, wl, wr, cin, cout, den, dm, st, raw);
+#endif
     switch (p->taps) {
 #define ASW_CASE(TT) \
     case TT:         \

@@ -481,6 +481,7 @@ const char *asw_strerror(int s) {
         case ASW_E_HIP: return "HIP runtime error";
         case ASW_E_NOMEM: return "out of memory";
         case ASW_E_UNSUPPORTED: return "unsupported parameter combination";
+        case ASW_E_COMM: return "collective (RCCL) error";
         default: return "unknown status";
     }
 }

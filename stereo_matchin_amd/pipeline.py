@@ -157,17 +157,49 @@ def to_rgba(img: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(np.concatenate([img[..., :3], a], axis=2))
 
 
-def match_frame(params: AswParams, left_rgba: np.ndarray, right_rgba: np.ndarray, device: int = 0,
-                want_cost: bool = False, refine=None) -> dict:
-    """Frame API (``asw_create`` + ``asw_match``): host RGBA8 in, host maps out."""
-    L = _lib.lib()
-    H, W = params.height, params.width
-    left_rgba = to_rgba(left_rgba)
-    right_rgba = to_rgba(right_rgba)
-    assert left_rgba.shape == (H, W, 4) and right_rgba.shape == (H, W, 4)
-    ctx = ctypes.c_void_p()
-    _lib.check(L.asw_create(ctypes.byref(params), device, ctypes.byref(ctx)), "asw_create")
-    try:
+class FrameContext:
+    """The FRAME API (``asw_create`` / ``asw_create_multi`` / ``asw_create_rank`` +
+    ``asw_match`` / ``asw_match_batch``): host RGBA8 in, host maps out, buffers
+    allocated once and reused pair after pair.
+
+    ``devices``: HIP ordinals of the shards driven by this process (one = one GPU;
+    several = the disparity range split across them, RCCL when distinct, a
+    device-local reduction when an ordinal repeats).  ``rank``/``nranks``/``comm_id``:
+    one process per GPU (``asw_create_rank``), ``comm_id`` from :func:`comm_unique_id`.
+    """
+
+    def __init__(self, params: AswParams, devices=(0,), rank: int | None = None, nranks: int | None = None,
+                 comm_id: bytes | None = None, refine=None):
+        self.L = _lib.lib()
+        self.p = params.copy()
+        self.ctx = ctypes.c_void_p()
+        devices = list(devices)
+        if rank is not None:
+            if len(devices) != 1 or comm_id is None or nranks is None:
+                raise ValueError("rank mode: one device, nranks and comm_id")
+            _lib.check(self.L.asw_create_rank(ctypes.byref(self.p), devices[0], rank, nranks, comm_id,
+                                              ctypes.byref(self.ctx)), "asw_create_rank")
+        elif len(devices) == 1:
+            _lib.check(self.L.asw_create(ctypes.byref(self.p), devices[0], ctypes.byref(self.ctx)), "asw_create")
+        else:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            _lib.check(self.L.asw_create_multi(ctypes.byref(self.p), arr, len(devices), ctypes.byref(self.ctx)),
+                       "asw_create_multi")
+        self.refine = refine is not None
+        if refine is not None:  # an AswRefineParams: main.cpp:540-623 inside asw_match
+            _lib.check(self.L.asw_set_refine(self.ctx, ctypes.byref(refine)), "asw_set_refine")
+
+    def shards(self) -> list[tuple[int, int]]:
+        n, b, e = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self.L.asw_ctx_shard(self.ctx, 0, ctypes.byref(n), None, None)
+        out = []
+        for i in range(n.value):
+            _lib.check(self.L.asw_ctx_shard(self.ctx, i, None, ctypes.byref(b), ctypes.byref(e)), "asw_ctx_shard")
+            out.append((b.value, e.value))
+        return out
+
+    def _outputs(self, want_cost: bool, want16: bool):
+        H, W = self.p.height, self.p.width
         out = {
             "d_ref": np.empty((H, W), np.int32), "d_tar": np.empty((H, W), np.int32),
             "conf_ref": np.empty((H, W), np.float32), "conf_tar": np.empty((H, W), np.float32),
@@ -175,18 +207,65 @@ def match_frame(params: AswParams, left_rgba: np.ndarray, right_rgba: np.ndarray
             "lr_red_rgba": np.empty((H, W, 4), np.uint8),
         }
         if want_cost:
-            out["cost"] = np.empty((H, W, _lib.disp_pitch(params)), np.float32)
-        if refine is not None:  # an AswRefineParams: main.cpp:540-623 inside asw_match
-            _lib.check(L.asw_set_refine(ctx, ctypes.byref(refine)), "asw_set_refine")
+            out["cost"] = np.zeros((H, W, _lib.disp_pitch(self.p)), np.float32)
+        if self.refine:
             out["final_rgba"] = np.empty((H, W, 4), np.uint8)
             out["post_red_rgba"] = np.empty((H, W, 4), np.uint8)
-        o = _lib.AswOutputs(*[out[k].ctypes.data if k in out else None for k in
-                              ("d_ref", "d_tar", "conf_ref", "conf_tar", "disp_rgba", "lr_rgba", "lr_red_rgba",
-                               "cost", "final_rgba", "post_red_rgba")])
-        t = _lib.AswTimings()
-        _lib.check(L.asw_match(ctx, left_rgba.ctypes.data, right_rgba.ctypes.data, ctypes.byref(o), ctypes.byref(t)),
-                   "asw_match")
-        out["timings"] = {f: getattr(t, f) for f, _ in t._fields_}
-        return out
-    finally:
-        L.asw_destroy(ctx)
+        if want16:
+            out["disp16"] = np.empty((H, W), np.uint16)
+            out["lr16"] = np.empty((H, W), np.uint16)
+        o = _lib.AswOutputs(*[out[k].ctypes.data if k in out else None for k, _ in _lib.AswOutputs._fields_])
+        return out, o
+
+    def match(self, left_rgba: np.ndarray, right_rgba: np.ndarray, want_cost: bool = False,
+              want16: bool = False) -> dict:
+        return self.match_batch(left_rgba[None], right_rgba[None], want_cost, want16)[0]
+
+    def match_batch(self, lefts: np.ndarray, rights: np.ndarray, want_cost: bool = False,
+                    want16: bool = False) -> list[dict]:
+        """``asw_match_batch``: lefts / rights are [B][H][W][4] (or RGB) stacks."""
+        H, W = self.p.height, self.p.width
+        lefts = np.ascontiguousarray(np.stack([to_rgba(x) for x in lefts]))
+        rights = np.ascontiguousarray(np.stack([to_rgba(x) for x in rights]))
+        B = lefts.shape[0]
+        assert lefts.shape == (B, H, W, 4) and rights.shape == (B, H, W, 4)
+        outs, os_ = zip(*[self._outputs(want_cost, want16) for _ in range(B)]) if B else ((), ())
+        oarr = (_lib.AswOutputs * B)(*os_)
+        tarr = (_lib.AswTimings * B)()
+        _lib.check(self.L.asw_match_batch(self.ctx, lefts.ctypes.data, rights.ctypes.data, B, oarr, tarr),
+                   "asw_match_batch")
+        for b in range(B):
+            outs[b]["timings"] = \
+                {f: getattr(tarr[b], f) for f, _ in tarr[b]._fields_}
+        return list(outs)
+
+    def close(self):
+        if self.ctx:
+            self.L.asw_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id() -> bytes:
+    """``asw_comm_unique_id`` (ncclGetUniqueId) for :class:`FrameContext` rank mode."""
+    buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+    _lib.check(_lib.lib().asw_comm_unique_id(buf), "asw_comm_unique_id")
+    return buf.raw
+
+
+def match_frame(params: AswParams, left_rgba: np.ndarray, right_rgba: np.ndarray, device: int = 0,
+                want_cost: bool = False, refine=None, devices=None, want16: bool = False) -> dict:
+    """Frame API (``asw_create`` + ``asw_match``): host RGBA8 in, host maps out."""
+    with FrameContext(params, devices=devices if devices is not None else (device,), refine=refine) as fc:
+        return fc.match(left_rgba, right_rgba, want_cost=want_cost, want16=want16)

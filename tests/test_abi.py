@@ -90,3 +90,32 @@ def test_stage_api_validates_before_launch(L):
     assert lib.asw_aggregate_pass_den(ctypes.byref(p), 0, 1, 1, 1, 2, 2, L.DEN_WRITE, None) == L.ASW_E_INVALID
     p.d_end = 30
     assert lib.asw_wta(ctypes.byref(p), 1, 1, 1, 1, 1, None, None, None) == L.ASW_E_INVALID  # sharded
+
+
+def test_pass_rejects_volumes_past_32bit_offsets(L):
+    # the pass kernels address up to ~2T+16 cost rows from a 32-bit buffer offset
+    # (ADVICE r01): such shapes return ASW_E_UNSUPPORTED before any launch
+    lib = L.lib()
+    p = L.default_params(7680, 64, ndisp=1280, taps=51)
+    assert L.params_check(p) == L.ASW_OK
+    assert lib.asw_aggregate_pass(ctypes.byref(p), 0, 1, 1, 1, 2, None) == L.ASW_E_UNSUPPORTED
+    assert lib.asw_aggregate_pass_den(ctypes.byref(p), 1, 1, 1, 1, 2, 3, L.DEN_WRITE, None) == L.ASW_E_UNSUPPORTED
+    # C5 (3840 x 2160, D 512, T 51) is inside the range; so are the supports (< 2 GiB)
+    q = L.default_params(3840, 2160, ndisp=512, taps=51)
+    assert 3840 * 512 * 4 * (2 * 51 + 16) < 2 ** 31
+    assert lib.asw_support_bytes(ctypes.byref(q)) < 2 ** 31
+
+
+def test_frame_api_validates_before_allocating(L):
+    lib = L.lib()
+    p = L.default_params(16, 8, ndisp=16, taps=5)
+    ctx = ctypes.c_void_p()
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert lib.asw_create_multi(ctypes.byref(p), devs, 0, ctypes.byref(ctx)) == L.ASW_E_INVALID
+    assert lib.asw_create_multi(ctypes.byref(p), None, 2, ctypes.byref(ctx)) == L.ASW_E_INVALID
+    assert lib.asw_create_rank(ctypes.byref(p), 0, 2, 2, b"\0" * 128, ctypes.byref(ctx)) == L.ASW_E_INVALID
+    p.d_end = 8  # contexts shard the disparity axis themselves
+    assert lib.asw_create(ctypes.byref(p), 0, ctypes.byref(ctx)) == L.ASW_E_INVALID
+    assert lib.asw_ctx_shard(None, 0, None, None, None) == L.ASW_E_INVALID
+    assert lib.asw_match_batch(None, None, None, 1, None, None) == L.ASW_E_INVALID
+    assert L.strerror(L.ASW_E_COMM)

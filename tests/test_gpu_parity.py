@@ -192,9 +192,33 @@ def test_raw_fused_first_v_pass(gpu, oracle, T, H, W, D, d0, d1, tau):
     assert np.array_equal(got, want)
 
 
-# every compiled pass variant (asw_tune_set): block shapes, 8-wave V, and the
-# diagonal-pair H kernel (Dp % 128 == 0), on shapes that hit segment / row edges
-@pytest.mark.parametrize("variant", [0, 8, 64, 128, 32, 34, 36, 40, 48])
+# V pass (k_vpass10) on images tall enough for its unclamped interior chunks
+# (rows well past 2T + the look-ahead), every den mode, a shard with padding planes
+@pytest.mark.parametrize("T", [5, 9, 35, 51])
+@pytest.mark.parametrize("H,W,D,d0,d1", [(150, 70, 64, 0, 64), (233, 37, 200, 10, 140)])
+def test_vpass_v10_bit_exact(gpu, oracle, T, H, W, D, d0, d1):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    Lh, Rh = _rand_pair(T * 7 + W, H, W, shift=5)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
+    Dp = K.cost_shape(p)[2]
+    rng = np.random.default_rng(T + H)
+    sl, sr = oracle.support(Lh, T, 0), oracle.support(Rh, T, 0)
+    wl, wr = K.asw_vSupport(p, _t(Lh, gpu)), K.asw_vSupport(p, _t(Rh, gpu))
+    den = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+    for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
+        cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+        want = oracle.aggregate_pass(sl, sr, cin, T, 0, d0=d0, d1=d1, plane_base=d0)
+        out = K.asw_vCostAggregation(p, wl, wr, _t(pixel_major(cin, Dp), gpu), den=den, den_mode=mode)
+        got = plane_major(_np(out), d1 - d0)
+        assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
+
+
+# every compiled pass variant (asw_tune_set): H block shapes, on shapes that hit
+# segment / row edges
+@pytest.mark.parametrize("variant", [0, 64])
 @pytest.mark.parametrize("H,W,D,d0,d1", [(9, 331, 256, 0, 256), (6, 47, 128, 0, 128), (5, 161, 300, 40, 168),
                                           (4, 400, 256, 128, 256)])
 def test_pass_variants_bit_exact(gpu, oracle, variant, H, W, D, d0, d1):
