@@ -1,11 +1,17 @@
 """Benchmark of the MI355X ASW stereo hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c1|c2|c3|c5] [--api stage|frame]
 
-One step = one disparity map per frame group: raw cost -> 4 support launches ->
-r x (V, H) aggregation passes -> WTA (+ target map) -> LR consistency, on a
-synthetic stereo pair already resident in HBM (main.cpp:463-537 minus the
-refinement loop, the span of SURVEY §8d).  N > 1 GPUs (one process per GPU,
+One step = one disparity map per frame group (C5: a batch of 8 pairs): raw cost
+-> 4 support launches -> r x (V, H) aggregation passes -> WTA (+ target map) ->
+LR consistency, on a synthetic stereo pair already resident in HBM
+(main.cpp:463-537 minus the refinement loop, the span of SURVEY §8d).  C1 is the
+reference's own Tsukuba pair (tests/golden/tsukuba.npz), D16 T5.
+
+``--api frame`` times the C-ABI drop-in instead (asw_create + asw_match, host
+RGBA8 in, host maps out, as main.cpp's replacement would call it): ``value``
+stays the device-resident rate (the sum of asw_match's own HIP-event spans,
+h2d end -> consistency end), the PCIe-inclusive wall rate is reported beside it.  N > 1 GPUs (one process per GPU,
 launched by torch.distributed.run) shard the disparity axis of a frame over a
 group of G ranks with RCCL MIN all-reduces for the WTA; G = plan_groups(D, N)
 keeps >= 64 planes per rank (the pass kernels' plane block), so D=256 runs one
@@ -13,13 +19,17 @@ frame on 2 or 4 GPUs ("scaling": "strong") and two concurrent frames, each
 d-sharded 4 ways, on 8 GPUs ("weak" from 4 to 8: the per-GPU share stays 1/4
 frame).  `value` counts every frame all groups finished.
 
-Rank 0 prints ONE JSON line.  ``roofline`` is the aggregation pass (the dominant
-kernel, 94 % of the reference's ASW time): algorithmic bytes per launch
-``8*n*S + 8*T*S`` (read + write the n local cost planes, read both support
-arrays) over the launch's average duration from HIP events recorded
-on the stream the passes run on, inside the timed region.  ``cpu_baseline`` is the
-CPU oracle (oracle/, a scalar-semantics C/OpenMP restatement of the reference
-kernels) timed on this host on a bounded strip of the same frame.
+Rank 0 prints ONE JSON line.  ``roofline`` is the dominant kernel: the V
+aggregation pass with cached denominators (k_vpass10, DEN_READ: r-1 of the 2r
+launches per frame, the largest share of the frame; the H pass is reported beside
+it).  achieved = algorithmic bytes per launch ``8*n*S + 8*T*S`` (read + write the
+n local cost planes, read both support arrays of the direction) over
+the launch's average duration from HIP events recorded on the stream the passes
+run on, inside the timed region.  ``traffic`` = that kernel's HBM bytes per
+launch from rocprofv3 PMC (profiles/traffic.json, tools/traffic_json.py).
+``cpu_baseline`` is the CPU oracle (oracle/, a scalar-semantics C/OpenMP
+restatement of the reference kernels) on this host: a full frame with every
+OpenMP thread (C5: a strip), and a 1-thread strip (median of 3).
 """
 from __future__ import annotations
 
@@ -40,10 +50,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 WORKLOADS = {
     # name: (W, H, D, T, iters, lr, description)
     "c4": (1920, 1080, 256, 35, 7, True, "C4 synthetic 1920x1080 d=256 win=35 r=7 + LR check"),
+    "c1": (384, 288, 16, 5, 7, True, "C1 Tsukuba 384x288 d=16 win=5 r=7 + LR check (the reference pair)"),
     "c2": (450, 375, 64, 35, 7, False, "C2-size synthetic 450x375 d=64 win=35 r=7"),
     "c3": (450, 375, 64, 35, 7, True, "C3-size synthetic 450x375 d=64 win=35 r=7 + LR check"),
-    "c5": (3840, 2160, 512, 51, 7, True, "C5 synthetic 3840x2160 d=512 win=51 r=7 + LR check (1 pair/step)"),
+    "c5": (3840, 2160, 512, 51, 7, True, "C5 synthetic 3840x2160 d=512 win=51 r=7 + native LR check, batch of 8 pairs"),
 }
+BATCH = {"c5": 8}  # pairs per step
 
 
 def parse():
@@ -52,7 +64,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-rows", type=int, default=128, help="rows of the frame timed on the CPU oracle (0: skip)")
+    ap.add_argument("--cpu-rows", type=int, default=0,
+                    help="rows of the frame timed on the CPU oracle with every thread (0: the full frame; C5: 96)")
+    ap.add_argument("--api", default="stage", choices=["stage", "frame"],
+                    help="stage: device-resident StereoMatcher; frame: the C-ABI asw_match (host buffers)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--group-size", type=int, default=0,
@@ -60,32 +75,83 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(Lh, Rh, D, T, iters, rows):
-    """Oracle (oracle/asw_oracle.c, OpenMP) on rows [0, rows) of the frame, scaled to a full frame."""
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(Lh, Rh, D, T, iters, rows, lr_mode):
+    """Oracle (oracle/asw_oracle.c, OpenMP): rows [0, rows) of the frame (the full
+    frame when rows >= H) with every OpenMP thread, and a 1-thread strip (median of
+    3), each scaled to one map.  The oracle is the reference's arithmetic restated in
+    C (the reference's own CPU path is OpenCL-on-CPU, which this image cannot run)."""
     from oracle import oracle as O
-    threads = O.set_threads(0)
     H = Lh.shape[0]
+
+    def timed(r):
+        Ls, Rs = np.ascontiguousarray(Lh[:r]), np.ascontiguousarray(Rh[:r])
+        t0 = time.perf_counter()
+        O.match(Ls, Rs, D, T, iters)
+        return time.perf_counter() - t0
+
+    threads = O.set_threads(0)
     rows = min(rows, H)
-    Ls, Rs = np.ascontiguousarray(Lh[:rows]), np.ascontiguousarray(Rh[:rows])
-    t0 = time.perf_counter()
-    O.match(Ls, Rs, D, T, iters)
-    dt = time.perf_counter() - t0
+    dt = timed(rows)
     frame_s = dt * H / rows
+    what = "the full frame" if rows == H else f"a {Lh.shape[1]}x{rows} strip (rows 0-{rows - 1}), scaled x{H}/{rows}"
+    # one thread: a strip sized to ~2 s, median of 3
+    r1 = max(4, min(H, int(rows * 2.0 / max(dt * threads, 1e-3))))
+    O.set_threads(1)
+    try:
+        t1 = sorted(timed(r1) for _ in range(3))[1]
+    finally:
+        O.set_threads(threads)
+    one_s = t1 * H / r1
     return {
         "value": round(1.0 / frame_s, 6), "unit": "maps/s", "cores": int(threads), "kind": "port",
-        "sample": f"{Lh.shape[1]}x{rows} strip (rows 0-{rows - 1}) of the same frame, full pipeline r={iters}, "
-                  f"{dt:.2f} s measured, scaled x{H}/{rows} to one map; {frame_s * 1000:.0f} ms/map",
+        "sample": f"{what}: full pipeline r={iters} (raw cost, supports, 2r passes, WTA + target, LR check), "
+                  f"{dt:.2f} s measured, {frame_s * 1000:.0f} ms/map",
+        "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+        "one_thread": {"value": round(1.0 / one_s, 6), "unit": "maps/s",
+                       "sample": f"{Lh.shape[1]}x{r1} strip, median of 3 runs ({t1:.2f} s), scaled x{H}/{r1}; "
+                                 f"{one_s * 1000:.0f} ms/map"},
     }
 
 
-def load_traffic(path, workload, n_gpus):
+def load_traffic(path, workload, n_gpus, kernel):
+    """Per-launch HBM bytes of `kernel` from profiles/traffic.json (rocprofv3 PMC)."""
     try:
         with open(path) as f:
             t = json.load(f)
-        e = t.get(f"{workload}_n{n_gpus}")
-        return None if e is None else e.get("hbm_bytes_per_pass")
+        e = t.get(f"{workload}_n{n_gpus}") or {}
+        k = e.get(kernel) or {}
+        return k.get("total_bytes")
     except (OSError, ValueError):
         return None
+
+
+def load_pairs(workload, W, H, D, n):
+    """n stereo pairs of the workload (RGBA8 [H][W][4]): the reference's Tsukuba pair
+    for C1 (tests/golden/tsukuba.npz, the committed fixture), synthetic otherwise."""
+    from stereo_matchin_amd.synthetic import make_pair
+    if workload == "c1":
+        z = np.load(os.path.join(HERE, "tests", "golden", "tsukuba.npz"))
+        a = np.full(z["left"].shape[:2] + (1,), 255, np.uint8)
+        L = np.ascontiguousarray(np.concatenate([z["left"], a], -1))
+        R = np.ascontiguousarray(np.concatenate([z["right"], a], -1))
+        assert L.shape == (H, W, 4)
+        return [(L, R)] * n
+    out = []
+    for i in range(n):
+        L, R, _ = make_pair(W, H, D, i)
+        out.append((L, R))
+        print(f"[bench] synthetic pair {i + 1}/{n} ready", file=sys.stderr, flush=True)
+    return out
 
 
 def main():
@@ -103,37 +169,56 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from stereo_matchin_amd import make_params
+    from stereo_matchin_amd import FrameContext, make_params
     from stereo_matchin_amd.distributed import ShardedStereoMatcher, plan_groups
     from stereo_matchin_amd.pipeline import StereoMatcher
-    from stereo_matchin_amd.synthetic import make_pair
 
     W, H, D, T, iters, lr, desc = WORKLOADS[args.workload]
+    batch = BATCH.get(args.workload, 1)
+    lr_mode = 1 if D > 256 else 0  # the 8-bit codes collide above 256 levels: compare indices
     G = args.group_size or plan_groups(D, world)
     if world % G != 0:
         raise SystemExit(f"--group-size {G} does not divide {world} ranks")
+    if args.api == "frame" and world > 1:
+        raise SystemExit("--api frame runs on one GPU (multi-GPU frame contexts: asw_create_multi / asw_create_rank)")
     groups, gid, grank = world // G, rank // G, rank % G
     pg = None
     if world > 1 and G > 1:
         # every rank creates every group, in the same order (torch.distributed rule)
         subs = [dist.new_group(list(range(g * G, (g + 1) * G))) for g in range(groups)]
         pg = subs[gid]
-    Lh, Rh, _ = make_pair(W, H, D, gid)  # one synthetic pair per group
-    L = torch.from_numpy(Lh).to(dev)
-    R = torch.from_numpy(Rh).to(dev)
-    p = make_params(W, H, ndisp=D, taps=T, iters=iters, lr_check=int(lr))
-    if G > 1:
-        m = ShardedStereoMatcher(p, grank, G, dev, group=pg)
-        nloc = m.p.d_stop - m.p.d_begin
-    else:
-        m = StereoMatcher(p, dev)
+    # one set of pairs per frame group (groups run different pairs)
+    pairs_h = load_pairs(args.workload, W, H, D, batch) if groups == 1 else \
+        [(L, R) for L, R in load_pairs(args.workload, W, H, D, batch * groups)][gid * batch:(gid + 1) * batch]
+    p = make_params(W, H, ndisp=D, taps=T, iters=iters, lr_check=int(lr), lr_mode=lr_mode)
+    frame = args.api == "frame"
+    if frame:
+        fc = FrameContext(p, devices=[local])
         nloc = D
+    else:
+        pairs = [(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)) for L, R in pairs_h]
+        if G > 1:
+            m = ShardedStereoMatcher(p, grank, G, dev, group=pg)
+            nloc = m.p.d_stop - m.p.d_begin
+        else:
+            m = StereoMatcher(p, dev)
+            nloc = D
+    spans = []  # frame API: asw_match's device-resident spans (ms)
 
     def step(events=None):
-        return m.match(L, R, events=events)
+        for b in range(batch):
+            if frame:
+                out = fc.match(*pairs_h[b])
+                spans.append(out["timings"])
+            else:
+                ev = [] if events is not None else None
+                m.match(*pairs[b], events=ev)
+                if events is not None:
+                    events.append(ev)
 
     for _ in range(args.warmup):
         step()
+    spans.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -142,36 +227,51 @@ def main():
     evs = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ev = []
-        step(ev)
-        evs.append(ev)
+        step(evs)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     torch.cuda.synchronize()
 
-    # per-launch aggregation-pass durations from the events around each pass
-    v_ms, h_ms, frame_ms = [], [], []
-    for ev in evs:
-        prev = dict(ev)["support"]
-        for name, e in ev:
-            if name in ("v", "h"):
-                (v_ms if name == "v" else h_ms).append(prev.elapsed_time(e))
-                prev = e
-        frame_ms.append(ev[0][1].elapsed_time(ev[-1][1]))
-    pass_ms = float(np.mean(v_ms + h_ms))
-    stats = torch.tensor([elapsed, pass_ms, float(np.mean(v_ms)), float(np.mean(h_ms))], dtype=torch.float64,
-                         device=dev)
+    # per-launch aggregation-pass durations from the events around each pass:
+    # iteration 0 writes the cached denominators (DEN_WRITE), iterations 1..r-1 read them
+    v_rd, h_rd, v_wr, h_wr, frame_ms = [], [], [], [], []
+    if frame:
+        for t in spans:
+            frame_ms.append(t["total"])
+            # asw_timings keeps the per-direction mean over the r passes of a frame
+            v_rd.append(t["v_pass_mean"])
+            h_rd.append(t["h_pass_mean"])
+    else:
+        for ev in evs:
+            prev = dict(ev)["support"]
+            it = {"v": 0, "h": 0}
+            for name, e in ev:
+                if name in ("v", "h"):
+                    ms = prev.elapsed_time(e)
+                    first = it[name] == 0
+                    {("v", True): v_wr, ("v", False): v_rd, ("h", True): h_wr, ("h", False): h_rd}[(name, first)].append(ms)
+                    it[name] += 1
+                    prev = e
+            frame_ms.append(ev[0][1].elapsed_time(ev[-1][1]))
+    mean = lambda xs: float(np.mean(xs)) if xs else float("nan")  # noqa: E731
+    all_pass = v_rd + h_rd + v_wr + h_wr
+    stats = torch.tensor([elapsed, mean(v_rd), mean(h_rd), mean(v_wr), mean(h_wr), mean(all_pass),
+                          float(np.sum(frame_ms))], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    elapsed, pass_ms, v_avg, h_avg = stats.tolist()
+    elapsed, v_avg, h_avg, vw_avg, hw_avg, pass_avg, span_sum = stats.tolist()
 
     if rank == 0:
         S = W * H
         bytes_per_pass = 8 * nloc * S + 8 * T * S
-        achieved = bytes_per_pass / (pass_ms * 1e-3) / 1e9
-        maps_per_s = groups * args.steps / elapsed
+        gbs = lambda ms: bytes_per_pass / (ms * 1e-3) / 1e9  # noqa: E731
+        n_maps = groups * args.steps * batch
+        maps_per_s = n_maps / (span_sum / 1e3) if frame else n_maps / elapsed
+        dom = "v" if (v_avg >= h_avg or h_avg != h_avg) else "h"
+        dom_ms = v_avg if dom == "v" else h_avg
+        kname = "k_vpass10<DM_READ>" if dom == "v" else "k_hpass9<DM_READ>"
         out = {
             "metric": METRIC,
             "value": round(maps_per_s, 4),
@@ -184,21 +284,34 @@ def main():
             "scaling": "strong" if groups == 1 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic",
+            "data": "reference Tsukuba pair" if args.workload == "c1" else "synthetic",
             "config": {"workload": desc, "width": W, "height": H, "ndisp": D, "taps": T, "iters": iters,
-                       "lr_check": lr, "local_planes": nloc, "frames_per_step": groups,
-                       "parallelism": (f"{groups} frame(s) per step, each d-sharded over {G} GPU(s)"
+                       "lr_check": lr, "lr_mode": "native" if lr_mode else "u8", "pairs_per_step": batch,
+                       "local_planes": nloc, "frames_per_step": groups * batch, "api": args.api,
+                       "parallelism": (f"{groups} frame group(s), each d-sharded over {G} GPU(s)"
                                        if world > 1 else "single GPU")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(args.traffic, args.workload, world),
-                         "kernel": "aggregation pass (k_vpass/k_hpass), mean over all V+H launches",
-                         "bytes_per_launch": bytes_per_pass, "avg_launch_ms": round(pass_ms, 4),
-                         "v_avg_ms": round(v_avg, 4), "h_avg_ms": round(h_avg, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(gbs(dom_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs(dom_ms) / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(args.traffic, args.workload, world, kname),
+                         "kernel": f"{kname}: {'V' if dom == 'v' else 'H'} aggregation pass reading cached "
+                                   f"denominators ({max(iters - 1, 0)} of the {2 * iters} launches per frame)",
+                         "bytes_per_launch": bytes_per_pass, "avg_launch_ms": round(dom_ms, 4),
+                         "v_read_ms": round(v_avg, 4), "v_read_frac": round(gbs(v_avg) / HBM_PEAK_GBS, 4),
+                         "h_read_ms": round(h_avg, 4), "h_read_frac": round(gbs(h_avg) / HBM_PEAK_GBS, 4),
+                         "v_write_ms": round(vw_avg, 4), "h_write_ms": round(hw_avg, 4),
+                         "all_pass_mean_ms": round(pass_avg, 4),
+                         "all_pass_frac": round(gbs(pass_avg) / HBM_PEAK_GBS, 4),
+                         "timing": "frame API: asw_timings per-direction means over all r passes" if frame else
+                                   "HIP events on the passes' stream inside the timed region"},
             "frame_ms_events": round(float(np.median(frame_ms)), 4),
         }
-        if world == 1 and not args.no_cpu and args.cpu_rows > 0:
-            out["cpu_baseline"] = cpu_baseline(Lh, Rh, D, T, iters, args.cpu_rows)
+        if frame:
+            out["pcie_inclusive"] = {"value": round(n_maps / elapsed, 4), "unit": "maps/s",
+                                     "note": "wall clock of asw_match incl. host->device upload and device->host "
+                                             "read-back of every output"}
+        if world == 1 and not args.no_cpu:
+            rows = args.cpu_rows or (96 if args.workload == "c5" else H)
+            out["cpu_baseline"] = cpu_baseline(*pairs_h[0], D, T, iters, rows, lr_mode)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

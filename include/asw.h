@@ -98,6 +98,11 @@ int asw_support_lut(const asw_params *p, float *lut, void *stream);
 int asw_support(const asw_params *p, int dir, const uint8_t *img_rgba, const float *lut, float *w,
                 void *stream);
 
+/* the four support arrays of a frame in one launch (asw_vSupport and asw_hSupport of
+ * both images, main.cpp:469-484): bit-identical to four asw_support calls. */
+int asw_support_all(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba, const float *lut,
+                    float *wvl, float *whl, float *wvr, float *whr, void *stream);
+
 /* CIELab extension (north star; the reference has no colour conversion, so this
  * is not reference-pinned: the oracle restates the same IEEE double sequence and
  * colorimetric known answers pin the conversion).  With p->color_space ==

@@ -126,6 +126,7 @@ SIGNATURES = {
     "asw_raw_cost": (I, [PP, P, P, P, P]),
     "asw_support_lut": (I, [PP, P, P]),
     "asw_support": (I, [PP, I, P, P, P, P]),
+    "asw_support_all": (I, [PP, P, P, P, P, P, P, P, P]),
     "asw_lab_bytes": (ctypes.c_size_t, [PP]),
     "asw_lab": (I, [PP, P, P, P]),
     "asw_support_lab": (I, [PP, I, P, P, P]),

@@ -401,10 +401,7 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         ASWCHK(asw_support_lab(p, ASW_DIR_H, s.lab_r, s.whr, st));
     } else {
         ASWCHK(asw_support_lut(p, s.lut, st));
-        ASWCHK(asw_support(p, ASW_DIR_V, s.left, s.lut, s.wvl, st));
-        ASWCHK(asw_support(p, ASW_DIR_H, s.left, s.lut, s.whl, st));
-        ASWCHK(asw_support(p, ASW_DIR_V, s.right, s.lut, s.wvr, st));
-        ASWCHK(asw_support(p, ASW_DIR_H, s.right, s.lut, s.whr, st));
+        ASWCHK(asw_support_all(p, s.left, s.right, s.lut, s.wvl, s.whl, s.wvr, s.whr, st));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0], st));
     for (int it = 0; it < p->iters; ++it) {

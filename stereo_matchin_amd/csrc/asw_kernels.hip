@@ -77,21 +77,33 @@ __global__ void k_support_lut(float *lut, int rows, float gamma_c, float gamma_g
 
 // ---------------------------------------------------------------------------
 // asw_Aggr (K/asw_aggr.cl:3-23): per-disparity absolute-difference cost.
-// One thread per (pixel, local plane); d fastest => coalesced stores.
+// Block = 4 waves on row blockIdx.y, 4*PPW consecutive pixels; the right-image
+// pixels they reach (columns x - d) are staged once in LDS, so each lane's four
+// planes d = 4q..4q+3 read LDS instead of four gathers; the left pixel is
+// wave-uniform.  Every store is a float4 per lane (1 KB per wave-instruction).
 // ---------------------------------------------------------------------------
+constexpr int kRawPPW = 8;                        // pixels per wave
+constexpr int kRawSpan = 4 * kRawPPW;              // pixels per block
 __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, const uchar4 *__restrict__ R,
                                                    float *__restrict__ cost, int W, int Dp, int nloc, int d_begin,
-                                                   float tau, int px_per_wave) {
-    // block = 4 waves on row blockIdx.y; a wave writes whole pixels, 4 planes per
-    // lane per store (float4): 1 KB per wave-instruction, no 64-bit index math.
+                                                   float tau) {
     using f4 = float __attribute__((ext_vector_type(4)));
+    extern __shared__ uchar4 rrow[];  // R[y][xr], xr in [xlo, x0 + kRawSpan)
     const int y = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uchar4 *Lrow = L + (long long)y * W, *Rrow = R + (long long)y * W;
+    const int x0 = blockIdx.x * kRawSpan;
+    const int xlo = x0 - (d_begin + Dp - 1);  // smallest x - d of the block (staged clamped to [0, W-1])
+    const int nr = kRawSpan + Dp - 1;
+    for (int t = threadIdx.x; t < nr; t += 256) {
+        const int xr = xlo + t;
+        rrow[t] = Rrow[xr < 0 ? 0 : (xr >= W ? W - 1 : xr)];
+    }
+    __syncthreads();
     const int nq = Dp >> 2;
-    const int x0 = (blockIdx.x * 4 + wave) * px_per_wave;
-    const int x1 = min(x0 + px_per_wave, W);
-    for (int x = x0; x < x1; ++x) {
+    const int xa = x0 + wave * kRawPPW;
+    const int xb = min(xa + kRawPPW, W);
+    for (int x = xa; x < xb; ++x) {
         const uchar4 l = Lrow[x];
         f4 *out = reinterpret_cast<f4 *>(cost + ((long long)y * W + x) * Dp);
         for (int q = lane; q < nq; q += 64) {
@@ -100,7 +112,7 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
             for (int j = 0; j < 4; ++j) {
                 const int k = 4 * q + j;
                 const int d = d_begin + k;
-                const uchar4 r = Rrow[x - d < 0 ? 0 : x - d];
+                const uchar4 r = rrow[x - d - xlo];  // = R(max(x-d, 0), y): the stage clamps
                 float sv = fabsf((float)l.x - (float)r.x) + fabsf((float)l.y - (float)r.y);
                 sv = sv + fabsf((float)l.z - (float)r.z);
                 v[j] = k < nloc ? fminf(sv, tau) : 0.0f;
@@ -113,18 +125,31 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
 // ---------------------------------------------------------------------------
 // asw_vSupport / asw_hSupport (K/asw_vsupport.cl:3-27, K/asw_hsupport.cl:3-28).
 // w[y][x][i] = LUT[|delta|][SAD(p,q)], q the i-th tap of p's 1-D window.
+// One thread = one pixel's group of 4 taps (a float4 store); blockIdx.z selects one
+// of up to four (image, direction) jobs, so the four arrays of a frame are one
+// launch with four independent gathers per thread in flight.
 // ---------------------------------------------------------------------------
-// Row y = blockIdx.y; thread t of the row covers (x, i) = (t / Tp, t % Tp), so
-// consecutive threads store consecutive floats; 32-bit index math only.
-__global__ __launch_bounds__(256) void k_support(const uchar4 *__restrict__ img, const float *__restrict__ lut,
-                                                 float *__restrict__ w, int W, int H, int T, int Tp, int dir) {
+struct SupportJobs {
+    const uchar4 *img[4];
+    float *w[4];
+    int dir[4];
+};
+__global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *__restrict__ lut, int W, int H,
+                                                 int T, int Tp) {
+    using f4 = float __attribute__((ext_vector_type(4)));
     const int y = blockIdx.y;
+    const int Q = Tp >> 2;
     const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= W * Tp) return;
-    const int x = t / Tp, i = t - x * Tp;
+    if (t >= W * Q) return;
+    const int x = t / Q, q = t - x * Q;
+    const uchar4 *__restrict__ img = jobs.img[blockIdx.z];
+    const int dir = jobs.dir[blockIdx.z];
     const int R = T / 2;
-    float v = 0.0f;
-    if (i < T) {
+    const uchar4 a = img[y * W + x];
+    f4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = 4 * q + j;
         int qx = x, qy = y, dist;
         if (dir == ASW_DIR_V) {
             qy = clampi(y + i - R, 0, H - 1);
@@ -133,12 +158,11 @@ __global__ __launch_bounds__(256) void k_support(const uchar4 *__restrict__ img,
             qx = clampi(x + i - R, 0, W - 1);
             dist = x > qx ? x - qx : qx - x;
         }
-        const uchar4 a = img[y * W + x];
         const uchar4 b = img[qy * W + qx];
         const int sad = abs((int)a.x - (int)b.x) + abs((int)a.y - (int)b.y) + abs((int)a.z - (int)b.z);
-        v = lut[dist * kLutWidth + sad];
+        v[j] = i < T ? lut[dist * kLutWidth + sad] : 0.0f;
     }
-    w[(long long)y * W * Tp + t] = v;
+    reinterpret_cast<f4 *>(jobs.w[blockIdx.z] + (long long)y * W * Tp)[t] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -512,11 +536,13 @@ size_t asw_lut_bytes(const asw_params *p) { return (size_t)(p->taps / 2 + 1) * k
 int asw_raw_cost(const asw_params *p, const uint8_t *left, const uint8_t *right, float *cost, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!left || !right || !cost) return ASW_E_INVALID;
-    const int ppw = 8;  // pixels per wave
-    const dim3 grid((unsigned)((p->width + 4 * ppw - 1) / (4 * ppw)), (unsigned)p->height);
-    hipLaunchKernelGGL(k_raw_cost, grid, dim3(256), 0, (hipStream_t)stream, reinterpret_cast<const uchar4 *>(left),
-                       reinterpret_cast<const uchar4 *>(right), cost, p->width, asw_disp_pitch(p),
-                       d_end_of(p) - p->d_begin, p->d_begin, p->tad_tau, ppw);
+    const int Dp = asw_disp_pitch(p);
+    const dim3 grid((unsigned)((p->width + kRawSpan - 1) / kRawSpan), (unsigned)p->height);
+    const size_t lds = (size_t)(kRawSpan + Dp - 1) * 4;
+    if (lds > 64 * 1024) return ASW_E_UNSUPPORTED;
+    hipLaunchKernelGGL(k_raw_cost, grid, dim3(256), lds, (hipStream_t)stream, reinterpret_cast<const uchar4 *>(left),
+                       reinterpret_cast<const uchar4 *>(right), cost, p->width, Dp, d_end_of(p) - p->d_begin,
+                       p->d_begin, p->tad_tau);
     return finish_launch();
 }
 
@@ -530,15 +556,40 @@ int asw_support_lut(const asw_params *p, float *lut, void *stream) {
     return finish_launch();
 }
 
+static int launch_support(const asw_params *p, const SupportJobs &jobs, int njobs, const float *lut, void *stream) {
+    const int Tp = asw_tap_pitch(p);
+    const dim3 grid((unsigned)((p->width * (Tp / 4) + 255) / 256), (unsigned)p->height, (unsigned)njobs);
+    hipLaunchKernelGGL(k_support, grid, dim3(256), 0, (hipStream_t)stream, jobs, lut, p->width, p->height, p->taps,
+                       Tp);
+    return finish_launch();
+}
+
 int asw_support(const asw_params *p, int dir, const uint8_t *img, const float *lut, float *w, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!img || !lut || !w || (dir != ASW_DIR_V && dir != ASW_DIR_H)) return ASW_E_INVALID;
     if (p->color_space != ASW_COLOR_RGB) return ASW_E_INVALID;  // LAB contexts: asw_support_lab
-    const int Tp = asw_tap_pitch(p);
-    const dim3 grid((unsigned)((p->width * Tp + 255) / 256), (unsigned)p->height);
-    hipLaunchKernelGGL(k_support, grid, dim3(256), 0, (hipStream_t)stream,
-                       reinterpret_cast<const uchar4 *>(img), lut, w, p->width, p->height, p->taps, Tp, dir);
-    return finish_launch();
+    SupportJobs jobs{};
+    jobs.img[0] = reinterpret_cast<const uchar4 *>(img);
+    jobs.w[0] = w;
+    jobs.dir[0] = dir;
+    return launch_support(p, jobs, 1, lut, stream);
+}
+
+int asw_support_all(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut, float *wvl,
+                    float *whl, float *wvr, float *whr, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!left || !right || !lut || !wvl || !whl || !wvr || !whr) return ASW_E_INVALID;
+    if (p->color_space != ASW_COLOR_RGB) return ASW_E_INVALID;
+    SupportJobs jobs{};
+    const uchar4 *img[4] = {reinterpret_cast<const uchar4 *>(left), reinterpret_cast<const uchar4 *>(left),
+                            reinterpret_cast<const uchar4 *>(right), reinterpret_cast<const uchar4 *>(right)};
+    float *w[4] = {wvl, whl, wvr, whr};
+    for (int j = 0; j < 4; ++j) {
+        jobs.img[j] = img[j];
+        jobs.w[j] = w[j];
+        jobs.dir[j] = (j & 1) ? ASW_DIR_H : ASW_DIR_V;
+    }
+    return launch_support(p, jobs, 4, lut, stream);
 }
 
 int asw_lab(const asw_params *p, const uint8_t *img, float *lab, void *stream) {

@@ -54,14 +54,14 @@ __global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost
                                                   int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
                                                   int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
                                                   uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar,
-                                                  int nwaves) {
+                                                  int nwaves, int per_xcd) {
     using f4 = float __attribute__((ext_vector_type(4)));
     __shared__ float tile_all[4][64 * kTilePitch];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     // XCD-aware: blocks b, b+8, b+16, ... run on one XCD; give each XCD a
-    // contiguous range of waves so its target gathers hit rows its L2 just streamed
-    const int per_xcd = (nwaves / 4 + 7) / 8;
+    // contiguous range of per_xcd blocks (4 waves each) so its target gathers hit
+    // rows its L2 just streamed
     const int wave_id = ((blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3)) * 4 + wv;
     if (wave_id >= nwaves) return;
     float *tile = tile_all[wv];
@@ -283,15 +283,15 @@ int launch_wta_scan(const asw_params *p, int mode, const float *cost, const floa
                     uint8_t *code_tar, hipStream_t st) {
     const long long S = (long long)p->width * p->height;
     const int nwaves = (int)((S + 63) / 64);
-    const int per_xcd = (nwaves / 4 + 7) / 8 + 1;
+    const int per_xcd = ((nwaves + 3) / 4 + 7) / 8;  // blocks of 4 waves per XCD, the grid is exactly 8 x per_xcd
     const unsigned nblocks = 8u * (unsigned)per_xcd;
     const int Dp = asw_disp_pitch(p);
     if (mode == 0)
         hipLaunchKernelGGL(k_wta_scan<0>, dim3(nblocks), dim3(256), 0, st, cost, p->width, p->height, Dp, p->ndisp,
-                           ref_l, ref_r, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, nwaves);
+                           ref_l, ref_r, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, nwaves, per_xcd);
     else
         hipLaunchKernelGGL(k_wta_scan<1>, dim3(nblocks), dim3(256), 0, st, cost, p->width, p->height, Dp, p->ndisp,
-                           ref_l, ref_r, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, nwaves);
+                           ref_l, ref_r, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, nwaves, per_xcd);
     return finish();
 }
 

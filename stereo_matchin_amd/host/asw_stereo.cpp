@@ -17,7 +17,13 @@
 //     0 = off), asw_disparity.png (refined + 3x3 median, main.cpp:619-623) and
 //     asw_consistency_post-reff.png (main.cpp:629-631);
 //   * errors are printed and the driver continues with the next pair, like ErCheck
-//     (main.cpp:27-30).
+//     (main.cpp:27-30);
+//   * beyond the reference: --devices I,J,... splits the disparity range of every
+//     pair across several GPUs (asw_create_multi: RCCL all-reduces for the WTA; a
+//     repeated id puts several shards on one GPU), and 16-bit disparity images
+//     (asw_wta_disparity16.png, asw_consistency16.png with 65535 = inconsistent) are
+//     written with --png16 and always when D > 256, where the 8-bit codes collide
+//     (the LR check then compares indices, ASW_LR_NATIVE).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -36,15 +42,16 @@ struct Options {
     std::string root;  // default: directory of pics
     std::string tsv;   // default: "<device name>.tsv" in the current directory
     int runs = 10, ndisp = 61, taps = 33, iters = 7, device = 0, refine = 6;
+    std::vector<int> devices;  // --devices: one context over several GPUs
     float gamma_c = -1.0f, gamma_g = -1.0f, tau = -1.0f;
-    bool lab = false, lr = true, native_lr = false;
+    bool lab = false, lr = true, native_lr = false, png16 = false;
 };
 
 void usage() {
     std::fprintf(stderr,
                  "usage: asw_stereo [--pics FILE] [--root DIR] [--runs N] [--ndisp D] [--taps T] [--iters R]\n"
                  "                  [--gamma-c G] [--gamma-g G] [--tau TAU] [--lab] [--no-lr] [--native-lr]\n"
-                 "                  [--refine K] [--device I] [--tsv FILE]\n");
+                 "                  [--refine K] [--device I | --devices I,J,...] [--png16] [--tsv FILE]\n");
 }
 
 bool parse(int argc, char **argv, Options &o) {
@@ -70,6 +77,18 @@ bool parse(int argc, char **argv, Options &o) {
         else if (a == "--gamma-c") { if (!(v = next("--gamma-c"))) return false; o.gamma_c = (float)std::atof(v); }
         else if (a == "--gamma-g") { if (!(v = next("--gamma-g"))) return false; o.gamma_g = (float)std::atof(v); }
         else if (a == "--tau") { if (!(v = next("--tau"))) return false; o.tau = (float)std::atof(v); }
+        else if (a == "--devices") {
+            if (!(v = next("--devices"))) return false;
+            o.devices.clear();
+            for (const char *q = v; *q;) {
+                char *end = nullptr;
+                const long d = std::strtol(q, &end, 10);
+                if (end == q) return false;
+                o.devices.push_back((int)d);
+                q = *end == ',' ? end + 1 : end;
+            }
+        }
+        else if (a == "--png16") o.png16 = true;
         else if (a == "--lab") o.lab = true;
         else if (a == "--no-lr") o.lr = false;
         else if (a == "--native-lr") o.native_lr = true;
@@ -118,8 +137,13 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "cannot read %s\n", o.pics.c_str());
         return 1;
     }
+    if (o.devices.empty()) o.devices.push_back(o.device);
     char devname[256] = "hip-device";
-    asw_device_name(o.device, devname, (int)sizeof devname);
+    asw_device_name(o.devices[0], devname, (int)sizeof devname);
+    if (o.devices.size() > 1) {
+        const size_t k = std::strlen(devname);
+        std::snprintf(devname + k, sizeof devname - k, " x%zu", o.devices.size());
+    }
     std::printf("\t- Device name: %s\n", devname);
     const std::string tsv_path = o.tsv.empty() ? std::string(devname) + ".tsv" : o.tsv;
     FILE *tsv = std::fopen(tsv_path.c_str(), "w");
@@ -150,16 +174,19 @@ int main(int argc, char **argv) {
         if (o.tau > 0) p.tad_tau = o.tau;
         p.color_space = o.lab ? ASW_COLOR_LAB : ASW_COLOR_RGB;
         p.lr_check = o.lr ? 1 : 0;
-        p.lr_mode = o.native_lr ? ASW_LR_NATIVE : ASW_LR_U8;
+        const bool wide = p.ndisp > 256;  // 8-bit codes collide: compare indices, write 16-bit images
+        p.lr_mode = (o.native_lr || wide) ? ASW_LR_NATIVE : ASW_LR_U8;
+        const bool png16 = o.png16 || wide;
         asw_ctx *ctx = nullptr;
-        int st = asw_create(&p, o.device, &ctx);
+        int st = o.devices.size() > 1 ? asw_create_multi(&p, o.devices.data(), (int)o.devices.size(), &ctx)
+                                      : asw_create(&p, o.devices[0], &ctx);
         if (st != ASW_OK) {
             std::fprintf(stderr, "%s: asw_create: %s (hip %d)\n", folder.c_str(), asw_strerror(st),
                          asw_last_hip_error());
             ++failures;
             continue;
         }
-        const bool refine = o.refine > 0 && p.lr_check;
+        const bool refine = o.refine > 0 && p.lr_check && o.devices.size() == 1 && !wide;
         if (refine) {
             asw_refine_params rp;
             asw_refine_params_default(&rp);
@@ -174,6 +201,7 @@ int main(int argc, char **argv) {
         }
         const size_t S = (size_t)p.width * p.height;
         std::vector<uint8_t> disp(S * 4), lr(S * 4), lr_red(S * 4), fin(S * 4), post(S * 4);
+        std::vector<uint16_t> disp16(png16 ? S : 0), lr16(png16 ? S : 0);
         asw_outputs out;
         std::memset(&out, 0, sizeof out);
         out.disp_rgba = disp.data();
@@ -181,10 +209,12 @@ int main(int argc, char **argv) {
         out.lr_red_rgba = lr_red.data();
         out.final_rgba = refine ? fin.data() : nullptr;
         out.post_red_rgba = refine ? post.data() : nullptr;
+        out.disp16 = png16 ? disp16.data() : nullptr;
+        out.lr16 = png16 && p.lr_check ? lr16.data() : nullptr;
         if (tsv) {
             std::fprintf(tsv, "\n%s - %s\n", devname, folder.c_str());
             std::fprintf(tsv, "id\taggr\tsupp_w\tv_aggr_mean\th_aggr_mean\ttotal aggregation\twta\tconsistency\t"
-                              "total\trefine\th2d\td2h\n");
+                              "total\trefine\th2d\td2h\texchange\n");
         }
         for (int run = 0; run < o.runs && st == ASW_OK; ++run) {
             asw_timings t;
@@ -194,9 +224,9 @@ int main(int argc, char **argv) {
             std::printf("run %d: total %.3f ms (aggregation %.3f, V %.3f, H %.3f per pass)\n", run, t.total,
                         t.aggregation_total, t.v_pass_mean, t.h_pass_mean);
             if (tsv)
-                std::fprintf(tsv, "%d\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\n",
+                std::fprintf(tsv, "%d\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\t%0.3f\n",
                              run, t.raw_cost, t.support, t.v_pass_mean, t.h_pass_mean, t.aggregation_total, t.wta,
-                             t.consistency, t.total, t.refine, t.h2d, t.d2h);
+                             t.consistency, t.total, t.refine, t.h2d, t.d2h, t.exchange);
         }
         asw_destroy(ctx);
         if (st != ASW_OK) {
@@ -218,6 +248,15 @@ int main(int argc, char **argv) {
             if (!p.lr_check && w.img != &disp) continue;
             if (!refine && (w.img == &fin || w.img == &post)) continue;
             e = asw_host::png_save(dir + "/" + w.name, w.img->data(), L.width, L.height, 4);
+            if (!e.empty()) {
+                std::fprintf(stderr, "%s: %s\n", folder.c_str(), e.c_str());
+                ++failures;
+            }
+        }
+        if (png16) {
+            e = asw_host::png_save16(dir + "/asw_wta_disparity16.png", disp16.data(), L.width, L.height);
+            if (e.empty() && p.lr_check)
+                e = asw_host::png_save16(dir + "/asw_consistency16.png", lr16.data(), L.width, L.height);
             if (!e.empty()) {
                 std::fprintf(stderr, "%s: %s\n", folder.c_str(), e.c_str());
                 ++failures;

@@ -237,8 +237,11 @@ std::string png_load(const std::string &path, Image &out) {
     return e.empty() ? e : path + ": " + e;
 }
 
-std::string png_encode(const uint8_t *data, unsigned w, unsigned h, int channels, std::vector<uint8_t> &out) {
-    if (!data || !w || !h || (channels != 1 && channels != 4)) return "bad image";
+namespace {
+// rows of bytes, `channels` = bytes per pixel (the filter's left neighbour
+// distance), colour type `ctype` at bit depth `depth`
+std::string encode_bytes(const uint8_t *data, unsigned w, unsigned h, int channels, int ctype, int depth,
+                         std::vector<uint8_t> &out) {
     const size_t stride = (size_t)w * channels;
     // per row: the filter (None or Paeth) with the smaller sum of |signed residuals|
     std::vector<uint8_t> raw(h * (stride + 1));
@@ -281,13 +284,40 @@ std::string png_encode(const uint8_t *data, unsigned w, unsigned h, int channels
         ihdr[i] = (uint8_t)(ww >> (24 - 8 * i));
         ihdr[4 + i] = (uint8_t)(hh >> (24 - 8 * i));
     }
-    ihdr[8] = 8;
-    ihdr[9] = channels == 4 ? 6 : 0;
+    ihdr[8] = (uint8_t)depth;
+    ihdr[9] = (uint8_t)ctype;
     ihdr[10] = ihdr[11] = ihdr[12] = 0;
     chunk("IHDR", ihdr, 13);
     chunk("IDAT", z.data(), z.size());
     chunk("IEND", nullptr, 0);
     return {};
+}
+}  // namespace
+
+std::string png_encode(const uint8_t *data, unsigned w, unsigned h, int channels, std::vector<uint8_t> &out) {
+    if (!data || !w || !h || (channels != 1 && channels != 4)) return "bad image";
+    return encode_bytes(data, w, h, channels, channels == 4 ? 6 : 0, 8, out);
+}
+
+std::string png_encode16(const uint16_t *data, unsigned w, unsigned h, std::vector<uint8_t> &out) {
+    if (!data || !w || !h) return "bad image";
+    std::vector<uint8_t> be((size_t)w * h * 2);  // PNG samples are big-endian
+    for (size_t i = 0; i < (size_t)w * h; ++i) {
+        be[2 * i] = (uint8_t)(data[i] >> 8);
+        be[2 * i + 1] = (uint8_t)(data[i] & 255);
+    }
+    return encode_bytes(be.data(), w, h, 2, 0, 16, out);
+}
+
+std::string png_save16(const std::string &path, const uint16_t *data, unsigned w, unsigned h) {
+    std::vector<uint8_t> buf;
+    std::string e = png_encode16(data, w, h, buf);
+    if (!e.empty()) return e;
+    FILE *fp = std::fopen(path.c_str(), "wb");
+    if (!fp) return "cannot write " + path;
+    const bool ok = std::fwrite(buf.data(), 1, buf.size(), fp) == buf.size();
+    std::fclose(fp);
+    return ok ? std::string() : "short write " + path;
 }
 
 std::string png_save(const std::string &path, const uint8_t *data, unsigned w, unsigned h, int channels) {

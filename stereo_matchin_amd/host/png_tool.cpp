@@ -1,6 +1,7 @@
 // png_tool — exercises png_io from the CPU tests (tests/test_host.py):
 //   png_tool decode IN.png OUT.raw   -> "W H" on stdout, RGBA8 bytes to OUT.raw
 //   png_tool encode IN.raw W H C OUT.png   (C = 1 grey8 or 4 RGBA8)
+//   png_tool encode16 IN.raw W H OUT.png   (host-order uint16 grey)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -37,6 +38,19 @@ int main(int argc, char **argv) {
         }
         return 0;
     }
-    std::fprintf(stderr, "usage: png_tool decode IN.png OUT.raw | encode IN.raw W H C OUT.png\n");
+    if (argc == 6 && !std::strcmp(argv[1], "encode16")) {
+        const unsigned w = (unsigned)std::atoi(argv[3]), h = (unsigned)std::atoi(argv[4]);
+        std::vector<uint16_t> buf((size_t)w * h);
+        FILE *f = std::fopen(argv[2], "rb");
+        if (!f || std::fread(buf.data(), 2, buf.size(), f) != buf.size()) return 1;
+        std::fclose(f);
+        const std::string e = asw_host::png_save16(argv[5], buf.data(), w, h);
+        if (!e.empty()) {
+            std::fprintf(stderr, "%s\n", e.c_str());
+            return 1;
+        }
+        return 0;
+    }
+    std::fprintf(stderr, "usage: png_tool decode IN.png OUT.raw | encode IN.raw W H C OUT.png | encode16 IN.raw W H OUT.png\n");
     return 2;
 }

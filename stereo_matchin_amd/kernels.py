@@ -105,6 +105,17 @@ def _support(p: AswParams, direction: int, img: torch.Tensor, lut: torch.Tensor 
     return out
 
 
+def support_all(p: AswParams, left: torch.Tensor, right: torch.Tensor, lut: torch.Tensor, wvl: torch.Tensor,
+                whl: torch.Tensor, wvr: torch.Tensor, whr: torch.Tensor) -> None:
+    """asw_vSupport + asw_hSupport of both images in one launch (``asw_support_all``)."""
+    for img in (left, right):
+        _expect(img, (p.height, p.width, 4), torch.uint8, "image")
+    for w in (wvl, whl, wvr, whr):
+        _expect(w, support_shape(p), torch.float32, "out")
+    _lib.check(_lib.lib().asw_support_all(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(lut), _ptr(wvl), _ptr(whl),
+                                          _ptr(wvr), _ptr(whr), _stream(left.device)), "asw_support_all")
+
+
 def lab_image(p: AswParams, img: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """CIELab (D65) of an RGBA8 image, float32 [H][W][4] = (L*, a*, b*, 0) (north-star extension)."""
     _expect(img, (p.height, p.width, 4), torch.uint8, "image")

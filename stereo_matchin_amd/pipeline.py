@@ -85,10 +85,8 @@ class StereoMatcher:
             K.support_lab(p, DIR_H, lab_r, out=self.whr)
             return
         K.support_lut(p, self.device, out=self.lut)
-        K.asw_vSupport(p, left, self.lut, out=self.wvl)
-        K.asw_hSupport(p, left, self.lut, out=self.whl)
-        K.asw_vSupport(p, right, self.lut, out=self.wvr)
-        K.asw_hSupport(p, right, self.lut, out=self.whr)
+        # asw_vSupport / asw_hSupport of both images (main.cpp:469-484) in one launch
+        K.support_all(p, left, right, self.lut, self.wvl, self.whl, self.wvr, self.whr)
 
     def aggregate(self, events: list | None = None, images: tuple | None = None):
         """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515).

@@ -90,6 +90,12 @@ def test_support(gpu, oracle, T):
             want = oracle.support(img, T, direction)
             assert np.array_equal(np.transpose(w[:, :, :T], (2, 0, 1)), want), (T, direction)
             assert (w[:, :, T:Tp] == 0).all()
+    # the four arrays in one launch (asw_support_all)
+    L, R = _t(Lh, gpu), _t(Rh, gpu)
+    ws = [K.new_support(p, gpu) for _ in range(4)]
+    K.support_all(p, L, R, K.support_lut(p, gpu), *ws)
+    for w, img, direction in zip(ws, (Lh, Lh, Rh, Rh), (0, 1, 0, 1)):
+        assert np.array_equal(np.transpose(_np(w)[:, :, :T], (2, 0, 1)), oracle.support(img, T, direction))
 
 
 @pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35, 51])
@@ -425,3 +431,51 @@ def test_c4_full_size_properties(gpu, oracle):
     Ls, Rs = np.ascontiguousarray(Lh[500:540]), np.ascontiguousarray(Rh[500:540])
     _, rs = _run(gpu, Ls, Rs, 256, 35, 2)
     _compare_e2e(rs, oracle.match(Ls, Rs, 256, 35, 2, want_cost=True), 256)
+
+
+# ------------------------------------------------------------------ full-size properties (C5)
+
+def test_c5_full_size_properties(gpu, oracle):
+    """3840x2160, D=512, T=51, r=7 (C5, one pair) with the native LR check: parity on a
+    full-width strip against the oracle, size-independent properties on the whole frame."""
+    import torch
+    from stereo_matchin_amd import StereoMatcher
+    from stereo_matchin_amd.synthetic import make_pair
+    W, H, D, T = 3840, 2160, 512, 51
+    Lh, Rh, gt = make_pair(W, H, D, 3)
+    p = _params(W, H, D, T, 7, lr_mode=1)
+    m = StereoMatcher(p, gpu)
+    L, R = _t(Lh, gpu), _t(Rh, gpu)
+    res = m.match(L, R)
+    d_ref, d_tar = res.d_ref.clone(), res.d_tar.clone()
+    dr = _np(d_ref)
+    assert dr.min() >= 0 and dr.max() < D and dr.max() > 256  # past the 8-bit code range
+    # the index map is the first argmin of the returned volume (row blocks bound memory)
+    for y0 in range(0, H, 270):
+        c = res.cost[y0:y0 + 270, :, :D]
+        mn = c.amin(-1, keepdim=True)
+        first = (c == mn).to(torch.uint8).argmax(-1)
+        assert torch.equal(first.int(), d_ref[y0:y0 + 270]), y0
+        del c, mn, first
+    # native LR check: red exactly where |d_ref - d_tar| > 1
+    red = _np(res.lr_red_rgba)
+    bad = (red[..., 0] == 255) & (red[..., 1] == 0) & (red[..., 2] == 0)
+    assert np.array_equal(bad, np.abs(dr - _np(d_tar)) > 1)
+    # determinism: the same context again gives the same bits
+    cost_sum = float(res.cost[:, :, :D].double().sum())
+    res2 = m.match(L, R)
+    assert torch.equal(res2.d_ref, d_ref) and torch.equal(res2.d_tar, d_tar)
+    assert float(res2.cost[:, :, :D].double().sum()) == cost_sum
+    # quality sanity on the synthetic ground truth (non-occluded interior)
+    inner = np.s_[60:-60, 600:-60]
+    assert (np.abs(dr[inner] - gt[inner]) <= 1).mean() > 0.6
+    del m, res, res2
+    torch.cuda.empty_cache()
+    # bit-exact parity on a full-width strip (3840 x 24 rows, r = 2 to bound the oracle)
+    Ls, Rs = np.ascontiguousarray(Lh[1000:1024]), np.ascontiguousarray(Rh[1000:1024])
+    _, rs = _run(gpu, Ls, Rs, D, T, 2, lr_mode=1)
+    want = oracle.match(Ls, Rs, D, T, 2, want_cost=True)
+    assert np.array_equal(_np(rs.d_ref), want["d_ref"]) and np.array_equal(_np(rs.d_tar), want["d_tar"])
+    got = plane_major(_np(rs.cost), D)
+    assert_cost_close(got, want["cost"])
+    assert np.array_equal(got, want["cost"])

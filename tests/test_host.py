@@ -157,6 +157,22 @@ def test_png_encode_round_trip(tools, tmp_path, channels):
     np.testing.assert_array_equal(back.reshape(img.shape), img)
 
 
+def test_png_encode16_round_trip(tools, tmp_path):
+    # 16-bit grey disparity maps (D > 256: the 8-bit codes collide)
+    rng = np.random.default_rng(16)
+    img = rng.integers(0, 65536, (29, 41), dtype=np.uint16)
+    img[:5] = 511
+    img[5, :] = 0xFFFF
+    raw = tmp_path / "in16.raw"
+    img.tofile(raw)
+    out = tmp_path / "o16.png"
+    r = subprocess.run([tools, "encode16", str(raw), "41", "29", str(out)], capture_output=True)
+    assert r.returncode == 0, r.stderr
+    im = PIL.open(out)
+    assert im.mode.startswith("I")
+    np.testing.assert_array_equal(np.asarray(im).astype(np.uint16), img)
+
+
 def test_cli_usage_errors(tmp_path):
     subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc")], check=True)
     subprocess.run(["make", "-s", "-C", os.path.join(PKG, "host")], check=True)
@@ -188,3 +204,28 @@ def test_cli_tsukuba_reproduces_reference_png(tmp_path):
     header = next(ln for ln in lines if ln.startswith("id\t"))
     rows = [ln for ln in lines if ln[:1].isdigit()]
     assert len(rows) == 2 and all(len(ln.split("\t")) == len(header.split("\t")) for ln in rows)
+
+
+@pytest.mark.gpu
+def test_cli_devices_and_png16(tmp_path):
+    """--devices 0,0 (two d-shards on one GPU, asw_create_multi) reproduces the one-GPU
+    images; --png16 writes the 16-bit disparity maps (d_ref; 65535 = LR-inconsistent)."""
+    L, R, dev_red = load_scene("tsukuba")
+    d = tmp_path / "tsukuba"
+    d.mkdir()
+    PIL.fromarray(L[..., :3]).save(d / "im1.png")
+    PIL.fromarray(R[..., :3]).save(d / "im5.png")
+    (tmp_path / "pics.txt").write_text("tsukuba/im1.png\ntsukuba/im5.png\n")
+    r = subprocess.run([CLI, "--pics", str(tmp_path / "pics.txt"), "--runs", "1", "--devices", "0,0", "--png16",
+                        "--refine", "0", "--tsv", str(tmp_path / "t.tsv")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    np.testing.assert_array_equal(np.asarray(PIL.open(d / "asw_consistency_pre-reff.png").convert("RGB")), dev_red)
+    d16 = np.asarray(PIL.open(d / "asw_wta_disparity16.png")).astype(np.int64)
+    c16 = np.asarray(PIL.open(d / "asw_consistency16.png")).astype(np.int64)
+    wta8 = np.asarray(PIL.open(d / "asw_wta_disparity.png").convert("L")).astype(np.int64)
+    assert d16.max() <= 60
+    np.testing.assert_array_equal((17 * d16 + 1) >> 2, wta8)  # the reference's round-half-down code
+    red = (dev_red[..., 0] == 255) & (dev_red[..., 1] == 0) & (dev_red[..., 2] == 0)
+    np.testing.assert_array_equal(c16 == 65535, red)
+    np.testing.assert_array_equal(c16[~red], d16[~red])

@@ -11,6 +11,7 @@
 #   pass        tools/pass_bench.py (den modes, default variant)
 #   pmc         rocprofv3 --pmc counter sets (one run each) over tools/pass_bench.py
 #   calib       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over tools/ubench/fetch_calib
+#   traffic     rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, over bench.py (C4 frame) -> $OUT/traffic
 #   cmd:STR     any other command (STR runs under bash with a 300 s limit)
 # Every GPU step runs under its own `timeout -k 10`; the first step that fails
 # (non-zero exit, crash, time limit) ends the script with its status.
@@ -74,6 +75,13 @@ for step in "$@"; do
             for c in FETCH_SIZE WRITE_SIZE; do
                 run 120 "calib_$c" rocprofv3 --pmc $c --output-format csv -d "$OUT/calib/$c" -o run -- \
                     tools/ubench/fetch_calib
+            done ;;
+        traffic)
+            i=0
+            for c in FETCH_SIZE WRITE_SIZE; do
+                i=$((i + 1))
+                run 300 "traffic_$c" rocprofv3 --pmc $c --output-format csv -d "$OUT/traffic/p$i" -o run -- \
+                    python3 bench.py --steps 2 --warmup 1 --no-cpu $args
             done ;;
         cmd) run 300 "cmd_$TAG" bash -c "$arg" ;;
         *) echo "unknown step $step"; exit 2 ;;

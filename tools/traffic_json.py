@@ -1,35 +1,37 @@
 """Fold rocprofv3 FETCH_SIZE / WRITE_SIZE runs of bench.py into profiles/traffic.json.
 
-    python tools/traffic_json.py gpurun_out/pmc_<tag> [--key c4_n1] [--out profiles/traffic.json]
+    python tools/traffic_json.py gpurun_out/<tag>/pmc [--key c4_n1] [--out profiles/traffic.json]
 
-Corrections per MI355X_MICROARCH.md (HBM section): the counters are in KB;
-FETCH_SIZE on gfx950 reports half the bytes of a 16-B-per-lane streaming read, so
-it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  The aggregation
-passes stream the cost volume with 16-B-per-lane loads and stores, which is the
-calibrated case.  Reported per launch, averaged over every k_vpass/k_hpass
-dispatch, like bench.py's `achieved`.
+<root>/p*/ hold one --pmc counter set each (tools/gpu.sh "pmc" step, or any
+directory of rocprofv3 CSVs).  Corrections, calibrated on this hardware for the
+kernels' own access shapes (tools/ubench/fetch_calib.hip, profiles/r02/calib.json):
+the counters are in KB; FETCH_SIZE reads exactly half the bytes of a coalesced
+streaming read, for 4-B/lane (the cost-volume loads) as for 16-B/lane loads, so
+it is doubled; WRITE_SIZE is exact for 4-B and 16-B/lane stores.
+
+Entries are per kernel and den mode, averaged over dispatches, keyed like
+bench.py's roofline.kernel: "k_vpass10<DM_READ>", "k_hpass9<DM_WRITE>", ...
 """
 import argparse
-import csv
-import glob
 import json
 import os
-import statistics
+import re
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import collect  # noqa: E402
+
+DM = {0: "DM_NONE", 1: "DM_WRITE", 2: "DM_READ"}
 
 
-def per_kernel(root, counter):
-    vals = {}
-    for f in glob.glob(os.path.join(root, counter, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            name = r["Kernel_Name"]
-            k = "k_vpass" if "k_vpass" in name else "k_hpass" if "k_hpass" in name else None
-            if k:
-                # one row per dispatch (values summed over instances by rocprofv3)
-                d = vals.setdefault(k, {})
-                d[r["Dispatch_Id"]] = d.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    return {k: statistics.mean(v.values()) * 1024.0 for k, v in vals.items()}
+def key_of(name: str):
+    """k_vpass10<35, 16, 2, 2> -> k_vpass10<DM_READ>; k_hpass9<35, 4, 40, 2> -> k_hpass9<DM_READ>."""
+    m = re.match(r"(k_vpass10|k_vpass9|k_hpass9)<([^>]*)>", name)
+    if not m:
+        return None
+    args = [a.strip() for a in m.group(2).split(",")]
+    dm = int(args[2]) if m.group(1).startswith("k_vpass") else int(args[3])
+    return f"{m.group(1)}<{DM[dm]}>"
 
 
 def main():
@@ -39,23 +41,23 @@ def main():
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "traffic.json"))
     a = ap.parse_args()
-    fetch = per_kernel(a.root, "FETCH_SIZE")
-    write = per_kernel(a.root, "WRITE_SIZE")
-    entry = {"source": a.root, "corrections": "FETCH_SIZE x2 (gfx950 16B/lane reads), KB->bytes"}
-    tot = []
-    for k in ("k_vpass", "k_hpass"):
-        if k in fetch and k in write:
-            r, w = 2 * fetch[k], write[k]
-            entry[k] = {"read_bytes": round(r), "write_bytes": round(w), "total_bytes": round(r + w)}
-            tot.append(r + w)
-    entry["hbm_bytes_per_pass"] = round(statistics.mean(tot)) if tot else None
+    raw = collect(a.root)
+    entry = {"source": a.root,
+             "corrections": "hbm_read = 2 x FETCH_SIZE x 1024, hbm_write = WRITE_SIZE x 1024 "
+                            "(calibrated: profiles/r02/calib.json)"}
+    for name, c in raw.items():
+        k = key_of(name)
+        if not k or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+            continue
+        r, w = 2 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
+        entry[k] = {"read_bytes": round(r), "write_bytes": round(w), "total_bytes": round(r + w)}
     try:
         data = json.load(open(a.out))
     except (OSError, ValueError):
         data = {}
     data[a.key] = entry
     json.dump(data, open(a.out, "w"), indent=1, sort_keys=True)
-    print(json.dumps({a.key: entry}))
+    print(json.dumps({a.key: entry}, indent=1))
 
 
 if __name__ == "__main__":
