@@ -55,6 +55,13 @@ WORKLOADS = {
     "c3": (450, 375, 64, 35, 7, True, "C3-size synthetic 450x375 d=64 win=35 r=7 + LR check"),
     "c5": (3840, 2160, 512, 51, 7, True, "C5 synthetic 3840x2160 d=512 win=51 r=7 + native LR check, batch of 8 pairs"),
 }
+for _scene, (_w, _h) in {"tsukuba": (384, 288), "cones": (450, 375), "teddy": (450, 375),
+                         "laundry": (450, 372), "art": (450, 359)}.items():
+    # the reference's own configuration on its own scenes (D61 T33 r7 k6 +
+    # median, main.cpp:176-178): the span its published "ASW total" times
+    WORKLOADS[f"ref-{_scene}"] = (_w, _h, 61, 33, 7, True,
+                                  f"reference {_scene} {_w}x{_h} d=61 win=33 r=7 + LR + refinement k=6 + median")
+REFINE = {k: 6 for k in WORKLOADS if k.startswith("ref-")}  # refinement iterations per workload
 BATCH = {"c5": 8}  # pairs per step
 
 
@@ -136,11 +143,12 @@ def load_traffic(path, workload, n_gpus, kernel):
 
 
 def load_pairs(workload, W, H, D, n):
-    """n stereo pairs of the workload (RGBA8 [H][W][4]): the reference's Tsukuba pair
-    for C1 (tests/golden/tsukuba.npz, the committed fixture), synthetic otherwise."""
+    """n stereo pairs of the workload (RGBA8 [H][W][4]): the reference's own pairs for C1
+    and ref-<scene> (tests/golden/<scene>.npz, the committed fixtures), synthetic otherwise."""
     from stereo_matchin_amd.synthetic import make_pair
-    if workload == "c1":
-        z = np.load(os.path.join(HERE, "tests", "golden", "tsukuba.npz"))
+    if workload == "c1" or workload.startswith("ref-"):
+        scene = "tsukuba" if workload == "c1" else workload[4:]
+        z = np.load(os.path.join(HERE, "tests", "golden", f"{scene}.npz"))
         a = np.full(z["left"].shape[:2] + (1,), 255, np.uint8)
         L = np.ascontiguousarray(np.concatenate([z["left"], a], -1))
         R = np.ascontiguousarray(np.concatenate([z["right"], a], -1))
@@ -204,6 +212,11 @@ def main():
             m = StereoMatcher(p, dev)
             nloc = D
     spans = []  # frame API: asw_match's device-resident spans (ms)
+    k_ref = REFINE.get(args.workload, 0)
+    if frame and k_ref:
+        from stereo_matchin_amd import _lib
+        fc.close()
+        fc = FrameContext(p, devices=[local], refine=_lib.default_refine_params(iters=k_ref))
 
     def step(events=None):
         for b in range(batch):
@@ -212,7 +225,13 @@ def main():
                 spans.append(out["timings"])
             else:
                 ev = [] if events is not None else None
-                m.match(*pairs[b], events=ev)
+                res = m.match(*pairs[b], events=ev)
+                if k_ref:  # main.cpp:540-623: k x (ref_v, ref_h, WTA_REF, LR) + 3x3 median
+                    from stereo_matchin_amd import _lib
+                    m.refine(res, *pairs[b], rp=_lib.default_refine_params(iters=k_ref))
+                    if ev is not None:
+                        from stereo_matchin_amd.pipeline import _record
+                        ev.append(("refine", _record()))
                 if events is not None:
                     events.append(ev)
 
@@ -236,10 +255,12 @@ def main():
 
     # per-launch aggregation-pass durations from the events around each pass:
     # iteration 0 writes the cached denominators (DEN_WRITE), iterations 1..r-1 read them
-    v_rd, h_rd, v_wr, h_wr, frame_ms = [], [], [], [], []
+    v_rd, h_rd, v_wr, h_wr, frame_ms, refine_ms = [], [], [], [], [], []
     if frame:
         for t in spans:
-            frame_ms.append(t["total"])
+            frame_ms.append(t["total"] + t["refine"])
+            if k_ref:
+                refine_ms.append(t["refine"])
             # asw_timings keeps the per-direction mean over the r passes of a frame
             v_rd.append(t["v_pass_mean"])
             h_rd.append(t["h_pass_mean"])
@@ -248,6 +269,8 @@ def main():
             prev = dict(ev)["support"]
             it = {"v": 0, "h": 0}
             for name, e in ev:
+                if name == "refine":
+                    refine_ms.append(dict(ev)["consistency"].elapsed_time(e))
                 if name in ("v", "h"):
                     ms = prev.elapsed_time(e)
                     first = it[name] == 0
@@ -284,7 +307,9 @@ def main():
             "scaling": "strong" if groups == 1 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "reference Tsukuba pair" if args.workload == "c1" else "synthetic",
+            "data": ("reference Tsukuba pair (tests/golden)" if args.workload == "c1" else
+                     f"reference {args.workload[4:]} pair (tests/golden)" if args.workload.startswith("ref-")
+                     else "synthetic"),
             "config": {"workload": desc, "width": W, "height": H, "ndisp": D, "taps": T, "iters": iters,
                        "lr_check": lr, "lr_mode": "native" if lr_mode else "u8", "pairs_per_step": batch,
                        "local_planes": nloc, "frames_per_step": groups * batch, "api": args.api,
@@ -305,6 +330,11 @@ def main():
                                    "HIP events on the passes' stream inside the timed region"},
             "frame_ms_events": round(float(np.median(frame_ms)), 4),
         }
+        if k_ref:
+            out["refine"] = {"iters": k_ref, "median_ms": round(float(np.median(refine_ms)), 4),
+                             "note": "refinement loop + 3x3 median inside each step (main.cpp:540-623); "
+                                     "frame_ms_events = raw cost -> median, the span of the reference's "
+                                     "published ASW total (main.cpp:707-708, BASELINE.md §1)"}
         if frame:
             out["pcie_inclusive"] = {"value": round(n_maps / elapsed, 4), "unit": "maps/s",
                                      "note": "wall clock of asw_match incl. host->device upload and device->host "
