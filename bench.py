@@ -172,10 +172,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (launch N>1 with torch.distributed.run)")
+    # ASW_BENCH_REHEARSAL=1: every rank on GPU 0 with the gloo backend (CUDA tensors
+    # staged through the host), to run the N > 1 code path on a one-GPU box; the
+    # numbers of such a run are not a scaling measurement
+    rehearsal = os.environ.get("ASW_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from stereo_matchin_amd import FrameContext, make_params
     from stereo_matchin_amd.distributed import ShardedStereoMatcher, plan_groups
@@ -193,7 +202,8 @@ def main():
     pg = None
     if world > 1 and G > 1:
         # every rank creates every group, in the same order (torch.distributed rule)
-        subs = [dist.new_group(list(range(g * G, (g + 1) * G))) for g in range(groups)]
+        subs = [dist.new_group(list(range(g * G, (g + 1) * G)), backend="gloo" if rehearsal else None)
+                for g in range(groups)]
         pg = subs[gid]
     # one set of pairs per frame group (groups run different pairs)
     pairs_h = load_pairs(args.workload, W, H, D, batch) if groups == 1 else \
