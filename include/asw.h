@@ -179,6 +179,22 @@ int asw_wta_finalize(const asw_params *p, const int64_t *key, const float *m2, c
                      const float *t2, int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar,
                      uint8_t *code_ref, uint8_t *code_tar, void *stream);
 
+/* ---- d-sharded asw_WTA_REF (K/asw_wta_ref.cl:2-68): the refinement loop's volume
+ * scan over a shard, the asw_wta_local protocol on the penalised values
+ * 0.085*den*|val - i| + C (ref_l / ref_r = asw_ref_h's [2][S] output of each view):
+ *   asw_wta_ref_local -> allreduce_min(key)
+ *   asw_wta_ref_target_local(key) -> allreduce_min(tkey) -> asw_wta_second(tar) -> allreduce_min(t2)
+ *   asw_wta_ref_finalize.
+ * The left second minimum is not exchanged: the reference's `confidence` receives the
+ * target confidence last (K/asw_wta_ref.cl:64-66).  Equals asw_wta_ref bit for bit. */
+int asw_wta_ref_local(const asw_params *p, const float *cost, const float *ref_l, int64_t *key, float *m1, float *m2,
+                      void *stream);
+int asw_wta_ref_target_local(const asw_params *p, const float *cost, const float *ref_r, const int64_t *key_ref,
+                             int64_t *tkey, float *t1, float *t2, void *stream);
+int asw_wta_ref_finalize(const asw_params *p, const int64_t *key, const int64_t *tkey, const float *t2,
+                         int32_t *d_ref, int32_t *d_tar, float *conf_ref, uint8_t *code_ref, uint8_t *code_tar,
+                         void *stream);
+
 /* ---- refinement loop (main.cpp:540-623): k x (asw_ref_v, asw_ref_h on both views,
  * asw_WTA_REF, Constistency), then the 3x3 Median -> asw_disparity.png ----
  * Whole-volume contexts only (d_begin = 0, d_end = ndisp), ndisp <= 256, ASW_LR_U8:
@@ -310,7 +326,9 @@ int asw_match(asw_ctx *ctx, const uint8_t *left_rgba, const uint8_t *right_rgba,
 int asw_match_batch(asw_ctx *ctx, const uint8_t *left_rgba, const uint8_t *right_rgba, int batch,
                     asw_outputs *out, asw_timings *t);
 /* turn the refinement loop on for later asw_match calls (rp = NULL or iters = 0:
- * off, the default).  Needs lr_check and a one-shard context.  asw_match then
+ * off, the default).  Needs lr_check.  On a multi-shard context the loop's volume
+ * scan (asw_WTA_REF) is d-sharded and exchanged like the WTA (asw_wta_ref_local
+ * protocol); the per-pixel stages run on the first shard.  asw_match then
  * fills final_rgba / post_red_rgba; every other output (d_ref, d_tar, conf_*,
  * disp_rgba, lr_rgba, lr_red_rgba, disp16, lr16) stays the pre-refinement result
  * (they are copied out before the loop updates its buffers in place). */

@@ -141,6 +141,9 @@ SIGNATURES = {
     "asw_wta_target_local": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_second": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_finalize": (I, [PP, P, P, P, P, P, P, P, P, P, P, P]),
+    "asw_wta_ref_local": (I, [PP, P, P, P, P, P, P]),
+    "asw_wta_ref_target_local": (I, [PP, P, P, P, P, P, P, P]),
+    "asw_wta_ref_finalize": (I, [PP, P, P, P, P, P, P, P, P, P]),
     "asw_refine_params_default": (None, [RP]),
     "asw_refine_params_check": (I, [PP, RP]),
     "asw_refine_lut_bytes": (ctypes.c_size_t, [RP]),

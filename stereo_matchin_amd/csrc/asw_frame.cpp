@@ -44,6 +44,7 @@ struct Shard {
     float *m1 = nullptr, *m2 = nullptr, *t1 = nullptr, *t2 = nullptr, *m2_g = nullptr, *t2_g = nullptr;
     ncclComm_t comm = nullptr;
     hipEvent_t ready = nullptr;  // COMM_LOCAL: this shard's operand is complete
+    float *ref_l = nullptr, *ref_r = nullptr;  // sharded refinement, shards > 0: the per-view estimates
 };
 
 }  // namespace
@@ -228,7 +229,8 @@ void free_shard(Shard &s) {
     if (s.stream == nullptr && s.left == nullptr) return;
     (void)hipSetDevice(s.device);
     void *bufs[] = {s.left, s.right, s.lut, s.lab_l, s.lab_r, s.wvl, s.wvr, s.whl, s.whr, s.c0, s.c1, s.den_v,
-                    s.den_h, s.key, s.key_g, s.tkey, s.tkey_g, s.m1, s.m2, s.t1, s.t2, s.m2_g, s.t2_g};
+                    s.den_h, s.key, s.key_g, s.tkey, s.tkey_g, s.m1, s.m2, s.t1, s.t2, s.m2_g, s.t2_g, s.ref_l,
+                    s.ref_r};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (s.comm) (void)ncclCommDestroy(s.comm);
@@ -449,6 +451,71 @@ int sharded_wta(asw_ctx *c) {
                             c->conf_tar, c->code_ref, c->code_tar, s0.stream);
 }
 
+// The refinement loop (main.cpp:540-617) + median on a d-sharded frame.  The
+// per-pixel stages (asw_ref_v / asw_ref_h, consistency, median) run on shard 0 (in
+// one process per GPU: on every rank, identically); the volume scan (asw_WTA_REF)
+// runs on every shard and is exchanged like the WTA: MIN all-reduces of the left
+// key, the target key and the target second minimum (asw_wta_ref_local protocol).
+int refine_sharded(asw_ctx *c) {
+    const asw_params *p = &c->p;
+    const asw_refine_params *rp = &c->rp;
+    const size_t S = frame_pixels(p);
+    Shard &s0 = c->sh[0];
+    hipStream_t st = s0.stream;
+    char *ws = static_cast<char *>(c->rws);
+    float *lut = reinterpret_cast<float *>(ws);
+    ws += (asw_refine_lut_bytes(rp) + 255) / 256 * 256;
+    float *vl = reinterpret_cast<float *>(ws), *vr = vl + 2 * S, *hl = vr + 2 * S, *hr = hl + 2 * S;
+    int32_t *dr = reinterpret_cast<int32_t *>(hr + 2 * S), *dt = dr + S;
+    uint8_t *kl = reinterpret_cast<uint8_t *>(dt + S);
+    HIPCHK(hipSetDevice(s0.device));
+    ASWCHK(asw_refine_lut(p, rp, lut, st));
+    for (int it = 0; it < rp->iters; ++it) {
+        HIPCHK(hipSetDevice(s0.device));
+        ASWCHK(asw_ref_v(p, rp, s0.left, c->est, 4, c->conf_ref, lut, vl, st));
+        ASWCHK(asw_ref_v(p, rp, s0.right, c->code_tar, 1, c->conf_tar, lut, vr, st));
+        ASWCHK(asw_ref_h(p, rp, s0.left, c->conf_ref, vl, lut, hl, st));
+        ASWCHK(asw_ref_h(p, rp, s0.right, c->conf_tar, vr, lut, hr, st));
+        for (int i = 1; i < c->n; ++i) {  // the estimates to the other shards' devices
+            Shard &s = c->sh[i];
+            HIPCHK(hipMemcpyPeerAsync(s.ref_l, s.device, hl, s0.device, 2 * S * 4, st));
+            HIPCHK(hipMemcpyPeerAsync(s.ref_r, s.device, hr, s0.device, 2 * S * 4, st));
+        }
+        if (c->n > 1) {
+            HIPCHK(hipEventRecord(c->red_done, st));
+            for (int i = 1; i < c->n; ++i) {
+                HIPCHK(hipSetDevice(c->sh[i].device));
+                HIPCHK(hipStreamWaitEvent(c->sh[i].stream, c->red_done, 0));
+            }
+        }
+        for (int i = 0; i < c->n; ++i) {
+            Shard &s = c->sh[i];
+            HIPCHK(hipSetDevice(s.device));
+            ASWCHK(asw_wta_ref_local(&s.p, s.c0, i ? s.ref_l : hl, s.key, s.m1, s.m2, s.stream));
+            HIPCHK(hipMemcpyAsync(s.key_g, s.key, S * 8, hipMemcpyDeviceToDevice, s.stream));
+        }
+        ASWCHK(allreduce_min<int64_t>(c, b_key_g, ncclInt64));
+        for (int i = 0; i < c->n; ++i) {
+            Shard &s = c->sh[i];
+            HIPCHK(hipSetDevice(s.device));
+            ASWCHK(asw_wta_ref_target_local(&s.p, s.c0, i ? s.ref_r : hr, s.key_g, s.tkey, s.t1, s.t2, s.stream));
+            HIPCHK(hipMemcpyAsync(s.tkey_g, s.tkey, S * 8, hipMemcpyDeviceToDevice, s.stream));
+        }
+        ASWCHK(allreduce_min<int64_t>(c, b_tkey_g, ncclInt64));
+        for (int i = 0; i < c->n; ++i) {
+            Shard &s = c->sh[i];
+            HIPCHK(hipSetDevice(s.device));
+            ASWCHK(asw_wta_second(&s.p, s.tkey_g, s.tkey, s.t1, s.t2, s.t2_g, s.stream));
+        }
+        ASWCHK(allreduce_min<float>(c, b_t2_g, ncclFloat32));
+        HIPCHK(hipSetDevice(s0.device));
+        ASWCHK(asw_wta_ref_finalize(&s0.p, s0.key_g, s0.tkey_g, s0.t2_g, dr, dt, c->conf_ref, kl, c->code_tar, st));
+        ASWCHK(asw_consistency(p, dr, dt, kl, c->code_tar, c->conf_ref, c->conf_tar, c->est, c->post_red, st));
+    }
+    HIPCHK(hipSetDevice(s0.device));
+    return asw_median3(p, c->est, 4, c->final_rgba, st);
+}
+
 int match_one(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, asw_outputs *o, asw_timings *t) {
     const asw_params *p = &c->p;
     const size_t S = frame_pixels(p);
@@ -517,8 +584,11 @@ int match_one(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
     const bool refine = c->refine && p->lr_check;
     if (refine) {  // main.cpp:540-617 on a copy of consistency_error
         HIPCHK(hipMemcpyAsync(c->est, c->lr, S * 4, hipMemcpyDeviceToDevice, st));
-        ASWCHK(asw_refine(&s0.p, &c->rp, s0.left, s0.right, s0.c0, c->est, c->code_tar, c->conf_ref, c->conf_tar,
-                          c->rws, c->post_red, c->final_rgba, nullptr, nullptr, st));
+        if (c->comm == COMM_NONE)
+            ASWCHK(asw_refine(&s0.p, &c->rp, s0.left, s0.right, s0.c0, c->est, c->code_tar, c->conf_ref,
+                              c->conf_tar, c->rws, c->post_red, c->final_rgba, nullptr, nullptr, st));
+        else
+            ASWCHK(refine_sharded(c));
     }
     HIPCHK(hipEventRecord(ev[e_ref], st));
     if (o && refine) {
@@ -627,9 +697,18 @@ int asw_set_refine(asw_ctx *c, const asw_refine_params *rp) {
     const int s = asw_refine_params_check(&c->p, rp);
     if (s != ASW_OK) return s;
     if (!c->p.lr_check) return ASW_E_INVALID;  // the loop starts from the consistency image
-    if (c->n > 1 || c->nranks > 1) return ASW_E_UNSUPPORTED;  // asw_refine reads the whole volume
-    HIPCHK(hipSetDevice(c->sh[0].device));
     const size_t S = frame_pixels(&c->p);
+    for (int i = 1; i < c->n; ++i) {  // sharded refinement: the estimates of both views on every shard
+        Shard &s = c->sh[i];
+        HIPCHK(hipSetDevice(s.device));
+        if (!s.ref_l) ASWCHK(dev_alloc(&s.ref_l, 2 * S * 4));
+        if (!s.ref_r) ASWCHK(dev_alloc(&s.ref_r, 2 * S * 4));
+    }
+    if (c->n > 1 && !c->red_done) {
+        HIPCHK(hipSetDevice(c->sh[0].device));
+        HIPCHK(hipEventCreateWithFlags(&c->red_done, hipEventDisableTiming));
+    }
+    HIPCHK(hipSetDevice(c->sh[0].device));
     const size_t ws = asw_refine_workspace_bytes(&c->p, rp);
     if (c->rws) (void)hipFree(c->rws);
     c->rws = nullptr;

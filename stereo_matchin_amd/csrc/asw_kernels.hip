@@ -278,18 +278,28 @@ __device__ __forceinline__ long long wta_pixel(int blocks_per_xcd) {
     return ((long long)xcd * blocks_per_xcd + m) * 4 + (threadIdx.x >> 6);
 }
 
+// asw_WTA_REF's scanned value (K/asw_wta_ref.cl:28): 0.085f * den * fabs(val - i) + cost,
+// left to right, uncontracted; i = the candidate's scan index
+__device__ __forceinline__ float ref_penalty(float a, float val, int i, float c) {
+    const float b = fabsf(val - (float)i);
+    return a * b + c;
+}
+
 // Target (right-view) scan of asw_WTA (K/asw_wta.cl:50-67): for i < md,
 // xq = max(0,x-i), b = md + xq - x (the bresenham() line of :3-9 always has
 // slope 1), candidate C[b][y][xq].  Only b in [b_lo, b_hi) (the local shard) is
 // visited; `index` is i so ties keep the smallest i like the sequential scan.
+// pen = true: asw_WTA_REF's target scan, value a*|val - i| + cost (K/asw_wta_ref.cl:39-57)
 __device__ __forceinline__ Top2 target_scan(const float *__restrict__ cost, int x, int y, int W, int Dp, int md,
-                                            int b_lo, int b_hi, int lane) {
+                                            int b_lo, int b_hi, int lane, bool pen = false, float a = 0.0f,
+                                            float val = 0.0f) {
     Top2 s{kInit, kInit, INT_MAX};
     for (int i = lane; i < md; i += 64) {
         const int xq = x - i < 0 ? 0 : x - i;
         const int b = md + xq - x;
         if (b >= b_lo && b < b_hi) {
-            const float t = cost[((long long)y * W + xq) * Dp + (b - b_lo)];
+            float t = cost[((long long)y * W + xq) * Dp + (b - b_lo)];
+            if (pen) t = ref_penalty(a, val, i, t);
             top2_update(s, t, i);
         }
     }
@@ -329,16 +339,24 @@ __device__ __forceinline__ long long make_key(float v, int idx) {
 }
 constexpr long long kNoKey = 0x7fffffffffffffffLL;
 
-// d-sharded left WTA, local half: planes [d_begin, d_end) of the shard.
+// d-sharded left WTA, local half: planes [d_begin, d_end) of the shard.  ref != NULL:
+// the refinement loop's asw_WTA_REF (penalised values; ref = [2][S] value / den planes)
 __global__ __launch_bounds__(256) void k_wta_local(const float *__restrict__ cost, int W, int H, int Dp, int bpx,
                                                    int d_begin, int nloc, long long *__restrict__ key,
-                                                   float *__restrict__ m1, float *__restrict__ m2) {
+                                                   float *__restrict__ m1, float *__restrict__ m2,
+                                                   const float *__restrict__ ref) {
     const int lane = threadIdx.x & 63;
     const long long p = wta_pixel(bpx);
-    if (p >= (long long)W * H) return;
+    const long long S = (long long)W * H;
+    if (p >= S) return;
     const float *cp = cost + p * Dp;
     Top2 s{kInit, kInit, INT_MAX};
-    for (int k = lane; k < nloc; k += 64) top2_update(s, cp[k], d_begin + k);
+    if (ref) {
+        const float a = 0.085f * ref[S + p], val = ref[p];
+        for (int k = lane; k < nloc; k += 64) top2_update(s, ref_penalty(a, val, d_begin + k, cp[k]), d_begin + k);
+    } else {
+        for (int k = lane; k < nloc; k += 64) top2_update(s, cp[k], d_begin + k);
+    }
     top2_wave_reduce(s);
     if (lane == 0) {
         key[p] = s.idx == INT_MAX ? kNoKey : make_key(s.m1, s.idx);
@@ -351,14 +369,16 @@ __global__ __launch_bounds__(256) void k_wta_target_local(const float *__restric
                                                           int d_begin, int d_end,
                                                           const long long *__restrict__ key_ref,
                                                           long long *__restrict__ tkey, float *__restrict__ t1,
-                                                          float *__restrict__ t2) {
+                                                          float *__restrict__ t2, const float *__restrict__ ref) {
     const int lane = threadIdx.x & 63;
     const long long p = wta_pixel(bpx);
-    if (p >= (long long)W * H) return;
+    const long long S = (long long)W * H;
+    if (p >= S) return;
     const int x = (int)(p % W), y = (int)(p / W);
     const long long kr = key_ref[p];
     const int md = kr == kNoKey ? 0 : (int)(unsigned)(kr & 0xffffffffLL);
-    const Top2 t = target_scan(cost, x, y, W, Dp, md, d_begin, d_end, lane);
+    const Top2 t = ref ? target_scan(cost, x, y, W, Dp, md, d_begin, d_end, lane, true, 0.085f * ref[S + p], ref[p])
+                       : target_scan(cost, x, y, W, Dp, md, d_begin, d_end, lane);
     if (lane == 0) {
         tkey[p] = t.idx == INT_MAX ? kNoKey : make_key(t.m1, t.idx);
         t1[p] = t.m1;
@@ -398,6 +418,33 @@ __global__ void k_wta_finalize(int W, int H, int D, const long long *__restrict_
     conf_ref[p] = (m2[p] - m1) / m2[p];
     d_tar[p] = mdr;
     conf_tar[p] = (t2[p] - tm1) / t2[p];
+    if (code_ref) code_ref[p] = (uint8_t)code_u8(md, D);
+    if (code_tar) code_tar[p] = (uint8_t)code_u8(mdr, D);
+}
+
+// asw_WTA_REF finalize (K/asw_wta_ref.cl:59-68): indices and codes as asw_WTA; the
+// kernel's `confidence` receives the left and then the TARGET confidence, so conf_ref
+// = the target confidence and the left second minimum is not needed.
+__global__ void k_wta_ref_finalize(int W, int H, int D, const long long *__restrict__ key,
+                                   const long long *__restrict__ tkey, const float *__restrict__ t2,
+                                   int32_t *__restrict__ d_ref, int32_t *__restrict__ d_tar,
+                                   float *__restrict__ conf_ref, uint8_t *__restrict__ code_ref,
+                                   uint8_t *__restrict__ code_tar) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (long long)W * H) return;
+    const int x = (int)(p % W);
+    const long long k = key[p], tk = tkey[p];
+    const int md = k == kNoKey ? 0 : (int)(unsigned)(k & 0xffffffffLL);
+    int mdr = md;
+    float tm1 = kInit;
+    if (tk != kNoKey) {
+        const int i = (int)(unsigned)(tk & 0xffffffffLL);
+        mdr = md + (x - i < 0 ? 0 : x - i) - x;
+        tm1 = __uint_as_float((unsigned)((unsigned long long)tk >> 32));
+    }
+    d_ref[p] = md;
+    d_tar[p] = mdr;
+    conf_ref[p] = (t2[p] - tm1) / t2[p];
     if (code_ref) code_ref[p] = (uint8_t)code_u8(md, D);
     if (code_tar) code_tar[p] = (uint8_t)code_u8(mdr, D);
 }
@@ -681,7 +728,7 @@ int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m
     const int bpx = (int)(((n + 3) / 4 + 7) / 8);
     hipLaunchKernelGGL(k_wta_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
                        p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p) - p->d_begin,
-                       reinterpret_cast<long long *>(key), m1, m2);
+                       reinterpret_cast<long long *>(key), m1, m2, nullptr);
     return finish_launch();
 }
 
@@ -693,7 +740,45 @@ int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *
     const int bpx = (int)(((n + 3) / 4 + 7) / 8);
     hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
                        p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p),
-                       reinterpret_cast<const long long *>(key_ref), reinterpret_cast<long long *>(tkey), t1, t2);
+                       reinterpret_cast<const long long *>(key_ref), reinterpret_cast<long long *>(tkey), t1, t2,
+                       nullptr);
+    return finish_launch();
+}
+
+int asw_wta_ref_local(const asw_params *p, const float *cost, const float *ref_l, int64_t *key, float *m1, float *m2,
+                      void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!cost || !ref_l || !key || !m1 || !m2) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
+    hipLaunchKernelGGL(k_wta_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
+                       p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p) - p->d_begin,
+                       reinterpret_cast<long long *>(key), m1, m2, ref_l);
+    return finish_launch();
+}
+
+int asw_wta_ref_target_local(const asw_params *p, const float *cost, const float *ref_r, const int64_t *key_ref,
+                             int64_t *tkey, float *t1, float *t2, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!cost || !ref_r || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
+    hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
+                       p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p),
+                       reinterpret_cast<const long long *>(key_ref), reinterpret_cast<long long *>(tkey), t1, t2,
+                       ref_r);
+    return finish_launch();
+}
+
+int asw_wta_ref_finalize(const asw_params *p, const int64_t *key, const int64_t *tkey, const float *t2,
+                         int32_t *d_ref, int32_t *d_tar, float *conf_ref, uint8_t *code_ref, uint8_t *code_tar,
+                         void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!key || !tkey || !t2 || !d_ref || !d_tar || !conf_ref) return ASW_E_INVALID;
+    const long long n = (long long)p->width * p->height;
+    hipLaunchKernelGGL(k_wta_ref_finalize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       p->width, p->height, p->ndisp, reinterpret_cast<const long long *>(key),
+                       reinterpret_cast<const long long *>(tkey), t2, d_ref, d_tar, conf_ref, code_ref, code_tar);
     return finish_launch();
 }
 

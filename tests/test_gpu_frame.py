@@ -156,3 +156,31 @@ def test_timings_for_many_iterations(gpu):
         t = fc.match(Lh, Rh)["timings"]
     for k in ("raw_cost", "support", "v_pass_mean", "h_pass_mean", "aggregation_total", "wta", "total"):
         assert t[k] > 0, k
+
+
+# the refinement loop on a d-sharded frame (its asw_WTA_REF scans exchanged like the
+# WTA): equal to the one-GPU refinement, which test_gpu_refine.py pins to the oracle
+@pytest.mark.parametrize("n", [2, 3])
+def test_multi_shard_refinement_equals_single(gpu, n):
+    from stereo_matchin_amd import FrameContext, _lib
+    Lh, Rh, _ = load_scene("tsukuba")
+    p = _p(Lh.shape[1], Lh.shape[0], 61, 33, 7)
+    rp = _lib.default_refine_params()
+    with FrameContext(p, devices=[0], refine=rp) as one:
+        ref = one.match(Lh, Rh)
+    with FrameContext(p, devices=[0] * n, refine=rp) as fc:
+        got = fc.match(Lh, Rh)
+    _same(got, ref, KEYS + ("final_rgba", "post_red_rgba"))
+    assert got["timings"]["refine"] > 0
+
+
+def test_rank_context_refinement(gpu):
+    from stereo_matchin_amd import FrameContext, _lib, comm_unique_id
+    Lh, Rh, _ = load_scene("cones")
+    p = _p(Lh.shape[1], Lh.shape[0], 64, 35, 2)
+    rp = _lib.default_refine_params(iters=3)
+    with FrameContext(p, devices=[0], refine=rp) as one:
+        ref = one.match(Lh, Rh)
+    with FrameContext(p, devices=[0], rank=0, nranks=1, comm_id=comm_unique_id(), refine=rp) as fc:
+        got = fc.match(Lh, Rh)
+    _same(got, ref, KEYS + ("final_rgba", "post_red_rgba"))
