@@ -75,6 +75,8 @@ def parse():
                     help="rows of the frame timed on the CPU oracle with every thread (0: the full frame; C5: 96)")
     ap.add_argument("--api", default="stage", choices=["stage", "frame"],
                     help="stage: device-resident StereoMatcher; frame: the C-ABI asw_match (host buffers)")
+    ap.add_argument("--graph", action="store_true",
+                    help="with --api frame: asw_set_graph (the device work replayed from HIP graphs)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--group-size", type=int, default=0,
@@ -211,7 +213,7 @@ def main():
     p = make_params(W, H, ndisp=D, taps=T, iters=iters, lr_check=int(lr), lr_mode=lr_mode)
     frame = args.api == "frame"
     if frame:
-        fc = FrameContext(p, devices=[local])
+        fc = FrameContext(p, devices=[local], graph=args.graph)
         nloc = D
     else:
         pairs = [(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)) for L, R in pairs_h]
@@ -226,7 +228,7 @@ def main():
     if frame and k_ref:
         from stereo_matchin_amd import _lib
         fc.close()
-        fc = FrameContext(p, devices=[local], refine=_lib.default_refine_params(iters=k_ref))
+        fc = FrameContext(p, devices=[local], refine=_lib.default_refine_params(iters=k_ref), graph=args.graph)
 
     def step(events=None):
         for b in range(batch):
@@ -271,6 +273,11 @@ def main():
             frame_ms.append(t["total"] + t["refine"])
             if k_ref:
                 refine_ms.append(t["refine"])
+        per_pass = spans
+        if args.graph:  # graph replays time only the coarse spans: passes from eager calls, outside the timed region
+            with FrameContext(p, devices=[local]) as eager:
+                per_pass = [eager.match(*pairs_h[0])["timings"] for _ in range(3)]
+        for t in per_pass:
             # asw_timings keeps the per-direction mean over the r passes of a frame
             v_rd.append(t["v_pass_mean"])
             h_rd.append(t["h_pass_mean"])
@@ -322,7 +329,8 @@ def main():
                      else "synthetic"),
             "config": {"workload": desc, "width": W, "height": H, "ndisp": D, "taps": T, "iters": iters,
                        "lr_check": lr, "lr_mode": "native" if lr_mode else "u8", "pairs_per_step": batch,
-                       "local_planes": nloc, "frames_per_step": groups * batch, "api": args.api,
+                       "local_planes": nloc, "frames_per_step": groups * batch,
+                       "api": args.api + ("+graph" if frame and args.graph else ""),
                        "parallelism": (f"{groups} frame group(s), each d-sharded over {G} GPU(s)"
                                        if world > 1 else "single GPU")},
             "roofline": {"bound": "hbm", "achieved": round(gbs(dom_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -333,6 +333,12 @@ int asw_match_batch(asw_ctx *ctx, const uint8_t *left_rgba, const uint8_t *right
  * disp_rgba, lr_rgba, lr_red_rgba, disp16, lr16) stays the pre-refinement result
  * (they are copied out before the loop updates its buffers in place). */
 int asw_set_refine(asw_ctx *ctx, const asw_refine_params *rp);
+/* on != 0: from the next asw_match on, the frame's device work (raw cost to the
+ * consistency images, and the refinement loop) is captured once into HIP graphs
+ * (hipStreamBeginCapture) and replayed: one launch per graph instead of ~25 (+37 for
+ * the loop) kernel launches, for small, launch-bound frames.  Same results.  Only
+ * the coarse timings (h2d, total, refine, d2h) are measured.  One-shard contexts. */
+int asw_set_graph(asw_ctx *ctx, int on);
 
 #ifdef __cplusplus
 }

@@ -155,6 +155,7 @@ SIGNATURES = {
     "asw_refine_workspace_bytes": (ctypes.c_size_t, [PP, RP]),
     "asw_refine": (I, [PP, RP, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "asw_set_refine": (I, [P, RP]),
+    "asw_set_graph": (I, [P, I]),
     "asw_tune_set": (I, [I, I]),
     "asw_device_name": (I, [I, ctypes.c_char_p, I]),
     "asw_create": (I, [PP, I, ctypes.POINTER(P)]),

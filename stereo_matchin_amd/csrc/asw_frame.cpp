@@ -70,6 +70,10 @@ struct asw_ctx {
     void *rws = nullptr;
     uint8_t *est = nullptr, *post_red = nullptr, *final_rgba = nullptr;  // RGBA8
     std::vector<hipEvent_t> ev;  // timing events on shard 0's stream
+    // asw_set_graph: the frame's device work captured once into HIP graphs, replayed
+    bool graph = false;
+    hipGraph_t g_main = nullptr, g_ref = nullptr;
+    hipGraphExec_t gx_main = nullptr, gx_ref = nullptr;
 };
 
 namespace {
@@ -295,6 +299,10 @@ int destroy_ctx(asw_ctx *c) {
     for (hipEvent_t e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->red_done) (void)hipEventDestroy(c->red_done);
+    if (c->gx_main) (void)hipGraphExecDestroy(c->gx_main);
+    if (c->gx_ref) (void)hipGraphExecDestroy(c->gx_ref);
+    if (c->g_main) (void)hipGraphDestroy(c->g_main);
+    if (c->g_ref) (void)hipGraphDestroy(c->g_ref);
     delete c;
     return ASW_OK;
 }
@@ -379,15 +387,18 @@ int create_ctx(const asw_params *p, const int *devs, int n, int shard0, int tota
 
 // raw cost + supports + 2r passes of one shard, asynchronous on its stream.
 // Pass-boundary events (timing) are recorded only for shard 0.
-int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *right_rgba, int e_raw, int e_pass0) {
+int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *right_rgba, int e_raw, int e_pass0,
+                    bool timing = true) {
     Shard &s = c->sh[i];
     const asw_params *p = &s.p;
     const size_t S = frame_pixels(p);
     hipStream_t st = s.stream;
-    const bool timed = i == 0;
+    const bool timed = i == 0 && timing;
     HIPCHK(hipSetDevice(s.device));
-    HIPCHK(hipMemcpyAsync(s.left, left_rgba, S * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(s.right, right_rgba, S * 4, hipMemcpyHostToDevice, st));
+    if (left_rgba) {  // NULL: the images are already on the device (graph replay)
+        HIPCHK(hipMemcpyAsync(s.left, left_rgba, S * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s.right, right_rgba, S * 4, hipMemcpyHostToDevice, st));
+    }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_raw], st));
     // the raw cost volume and the first V pass as two kernels: fusing asw_Aggr into
     // that pass (asw_aggregate_pass_raw) is bit-identical but measured slower on
@@ -516,6 +527,57 @@ int refine_sharded(asw_ctx *c) {
     return asw_median3(p, c->est, 4, c->final_rgba, st);
 }
 
+// The device work of a one-shard frame from uploaded images to the consistency
+// images (no events): what asw_set_graph captures into one HIP graph.
+int main_work_untimed(asw_ctx *c) {
+    const asw_params *p = &c->p;
+    const size_t S = frame_pixels(p);
+    Shard &s0 = c->sh[0];
+    hipStream_t st = s0.stream;
+    ASWCHK(shard_aggregate(c, 0, nullptr, nullptr, 1, 3, false));
+    ASWCHK(asw_wta(&s0.p, s0.c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar, st));
+    hipLaunchKernelGGL(k_codes_to_rgba, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, (long long)S,
+                       c->code_ref, reinterpret_cast<uchar4 *>(c->disp));
+    HIPCHK(hipGetLastError());
+    if (p->lr_check)
+        ASWCHK(asw_consistency(p, c->d_ref, c->d_tar, c->code_ref, c->code_tar, c->conf_ref, c->conf_tar, c->lr,
+                               c->lr_red, st));
+    hipLaunchKernelGGL(k_disp16, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, (long long)S, p->ndisp,
+                       p->lr_mode, p->lr_check, c->d_ref, c->d_tar, c->code_ref, c->code_tar, c->disp16, c->lr16);
+    HIPCHK(hipGetLastError());
+    return ASW_OK;
+}
+
+int refine_work(asw_ctx *c) {
+    const size_t S = frame_pixels(&c->p);
+    Shard &s0 = c->sh[0];
+    hipStream_t st = s0.stream;
+    HIPCHK(hipMemcpyAsync(c->est, c->lr, S * 4, hipMemcpyDeviceToDevice, st));
+    if (c->comm == COMM_NONE)
+        return asw_refine(&s0.p, &c->rp, s0.left, s0.right, s0.c0, c->est, c->code_tar, c->conf_ref, c->conf_tar,
+                          c->rws, c->post_red, c->final_rgba, nullptr, nullptr, st);
+    return refine_sharded(c);
+}
+
+// capture fn's work on stream st into *g / *gx (once), then launch it
+template <class F>
+int graph_run(hipStream_t st, hipGraph_t *g, hipGraphExec_t *gx, F &&fn) {
+    if (!*gx) {
+        HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        const int s = fn();
+        hipGraph_t cap = nullptr;
+        const hipError_t e = hipStreamEndCapture(st, &cap);
+        if (s != ASW_OK || e != hipSuccess) {
+            if (cap) (void)hipGraphDestroy(cap);
+            return s != ASW_OK ? s : hip_fail(e);
+        }
+        *g = cap;
+        HIPCHK(hipGraphInstantiate(gx, cap, nullptr, nullptr, 0));
+    }
+    HIPCHK(hipGraphLaunch(*gx, st));
+    return ASW_OK;
+}
+
 int match_one(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, asw_outputs *o, asw_timings *t) {
     const asw_params *p = &c->p;
     const size_t S = frame_pixels(p);
@@ -527,31 +589,40 @@ int match_one(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
     // then exchange end, wta end, consistency end, pre-refinement d2h end, refine end, d2h end
     const int e_pass0 = 3, e_x = e_pass0 + 2 * r + 1, e_wta = e_x + 1, e_cons = e_x + 2, e_pre = e_x + 3,
               e_ref = e_x + 4, e_d2h = e_x + 5;
+    const bool graphed = c->graph && c->comm == COMM_NONE;
     HIPCHK(hipSetDevice(s0.device));
     HIPCHK(hipEventRecord(ev[0], st));
-    for (int i = 0; i < c->n; ++i) ASWCHK(shard_aggregate(c, i, left_rgba, right_rgba, 1, e_pass0));
-    if (c->comm == COMM_NONE) {
-        HIPCHK(hipSetDevice(s0.device));
-        HIPCHK(hipEventRecord(ev[e_x], st));
-        ASWCHK(asw_wta(&s0.p, s0.c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar, st));
+    if (graphed) {
+        HIPCHK(hipMemcpyAsync(s0.left, left_rgba, S * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s0.right, right_rgba, S * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(ev[1], st));
+        ASWCHK(graph_run(st, &c->g_main, &c->gx_main, [&] { return main_work_untimed(c); }));
     } else {
-        ASWCHK(sharded_wta(c));
-        HIPCHK(hipSetDevice(s0.device));
-        HIPCHK(hipEventRecord(ev[e_x], st));
-    }
-    HIPCHK(hipEventRecord(ev[e_wta], st));
-    hipLaunchKernelGGL(k_codes_to_rgba, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, (long long)S,
-                       c->code_ref, reinterpret_cast<uchar4 *>(c->disp));
-    HIPCHK(hipGetLastError());
-    if (p->lr_check)
-        ASWCHK(asw_consistency(p, c->d_ref, c->d_tar, c->code_ref, c->code_tar, c->conf_ref, c->conf_tar, c->lr,
-                               c->lr_red, st));
-    const bool want16 = o && (o->disp16 || o->lr16);
-    if (want16) {
-        hipLaunchKernelGGL(k_disp16, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, (long long)S, p->ndisp,
-                           p->lr_mode, p->lr_check, c->d_ref, c->d_tar, c->code_ref, c->code_tar, c->disp16,
-                           c->lr16);
+        for (int i = 0; i < c->n; ++i) ASWCHK(shard_aggregate(c, i, left_rgba, right_rgba, 1, e_pass0));
+        if (c->comm == COMM_NONE) {
+            HIPCHK(hipSetDevice(s0.device));
+            HIPCHK(hipEventRecord(ev[e_x], st));
+            ASWCHK(asw_wta(&s0.p, s0.c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar,
+                           st));
+        } else {
+            ASWCHK(sharded_wta(c));
+            HIPCHK(hipSetDevice(s0.device));
+            HIPCHK(hipEventRecord(ev[e_x], st));
+        }
+        HIPCHK(hipEventRecord(ev[e_wta], st));
+        hipLaunchKernelGGL(k_codes_to_rgba, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, (long long)S,
+                           c->code_ref, reinterpret_cast<uchar4 *>(c->disp));
         HIPCHK(hipGetLastError());
+        if (p->lr_check)
+            ASWCHK(asw_consistency(p, c->d_ref, c->d_tar, c->code_ref, c->code_tar, c->conf_ref, c->conf_tar, c->lr,
+                                   c->lr_red, st));
+        const bool want16 = o && (o->disp16 || o->lr16);
+        if (want16) {
+            hipLaunchKernelGGL(k_disp16, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, (long long)S,
+                               p->ndisp, p->lr_mode, p->lr_check, c->d_ref, c->d_tar, c->code_ref, c->code_tar,
+                               c->disp16, c->lr16);
+            HIPCHK(hipGetLastError());
+        }
     }
     HIPCHK(hipEventRecord(ev[e_cons], st));
     // pre-refinement outputs leave before the loop updates its buffers in place
@@ -583,12 +654,8 @@ int match_one(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
     HIPCHK(hipEventRecord(ev[e_pre], st));
     const bool refine = c->refine && p->lr_check;
     if (refine) {  // main.cpp:540-617 on a copy of consistency_error
-        HIPCHK(hipMemcpyAsync(c->est, c->lr, S * 4, hipMemcpyDeviceToDevice, st));
-        if (c->comm == COMM_NONE)
-            ASWCHK(asw_refine(&s0.p, &c->rp, s0.left, s0.right, s0.c0, c->est, c->code_tar, c->conf_ref,
-                              c->conf_tar, c->rws, c->post_red, c->final_rgba, nullptr, nullptr, st));
-        else
-            ASWCHK(refine_sharded(c));
+        if (graphed) ASWCHK(graph_run(st, &c->g_ref, &c->gx_ref, [&] { return refine_work(c); }));
+        else ASWCHK(refine_work(c));
     }
     HIPCHK(hipEventRecord(ev[e_ref], st));
     if (o && refine) {
@@ -603,7 +670,13 @@ int match_one(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
         HIPCHK(hipStreamSynchronize(c->sh[i].stream));
     }
     HIPCHK(hipSetDevice(s0.device));
-    if (t) {
+    if (t && graphed) {  // one graph: only the coarse spans are measured
+        std::memset(t, 0, sizeof(*t));
+        t->h2d = ms_between(ev[0], ev[1]);
+        t->total = ms_between(ev[1], ev[e_cons]);
+        t->refine = refine ? ms_between(ev[e_pre], ev[e_ref]) : 0.0;
+        t->d2h = ms_between(ev[e_cons], ev[e_pre]) + ms_between(ev[e_ref], ev[e_d2h]);
+    } else if (t) {
         std::memset(t, 0, sizeof(*t));
         t->h2d = ms_between(ev[0], ev[1]);
         t->raw_cost = ms_between(ev[1], ev[2]);
@@ -718,6 +791,19 @@ int asw_set_refine(asw_ctx *c, const asw_refine_params *rp) {
     if (!c->final_rgba) ASWCHK(dev_alloc(&c->final_rgba, S * 4));
     c->rp = *rp;
     c->refine = true;
+    if (c->gx_ref) {  // the captured loop used the previous workspace / parameters
+        (void)hipGraphExecDestroy(c->gx_ref);
+        (void)hipGraphDestroy(c->g_ref);
+        c->gx_ref = nullptr;
+        c->g_ref = nullptr;
+    }
+    return ASW_OK;
+}
+
+int asw_set_graph(asw_ctx *c, int on) {
+    if (!c) return ASW_E_INVALID;
+    if (on && c->comm != COMM_NONE) return ASW_E_UNSUPPORTED;  // one shard, one stream
+    c->graph = on != 0;
     return ASW_OK;
 }
 

@@ -167,7 +167,7 @@ class FrameContext:
     """
 
     def __init__(self, params: AswParams, devices=(0,), rank: int | None = None, nranks: int | None = None,
-                 comm_id: bytes | None = None, refine=None):
+                 comm_id: bytes | None = None, refine=None, graph: bool = False):
         self.L = _lib.lib()
         self.p = params.copy()
         self.ctx = ctypes.c_void_p()
@@ -186,6 +186,8 @@ class FrameContext:
         self.refine = refine is not None
         if refine is not None:  # an AswRefineParams: main.cpp:540-623 inside asw_match
             _lib.check(self.L.asw_set_refine(self.ctx, ctypes.byref(refine)), "asw_set_refine")
+        if graph:  # asw_set_graph: capture the device work into HIP graphs, replay them
+            _lib.check(self.L.asw_set_graph(self.ctx, 1), "asw_set_graph")
 
     def shards(self) -> list[tuple[int, int]]:
         n, b, e = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

@@ -184,3 +184,18 @@ def test_rank_context_refinement(gpu):
     with FrameContext(p, devices=[0], rank=0, nranks=1, comm_id=comm_unique_id(), refine=rp) as fc:
         got = fc.match(Lh, Rh)
     _same(got, ref, KEYS + ("final_rgba", "post_red_rgba"))
+
+
+# asw_set_graph: the device work captured once into HIP graphs and replayed; every
+# output equals the eager path's, also for a second pair through the same graphs
+def test_graph_mode_equals_eager(gpu):
+    from stereo_matchin_amd import FrameContext, _lib
+    p = _p(450, 375, 64, 35, 3)
+    rp = _lib.default_refine_params(iters=2)
+    scenes = [load_scene("cones")[:2], load_scene("teddy")[:2]]
+    with FrameContext(p, refine=rp) as eager, FrameContext(p, refine=rp, graph=True) as graphed:
+        for Lh, Rh in scenes + scenes[:1]:
+            a = eager.match(Lh, Rh, want16=True)
+            b = graphed.match(Lh, Rh, want16=True)
+            _same(b, a, KEYS + ("final_rgba", "post_red_rgba", "disp16", "lr16"))
+            assert b["timings"]["total"] > 0 and b["timings"]["refine"] > 0
