@@ -188,6 +188,8 @@ __global__ __launch_bounds__(256) void k_ref_v(const uchar4 *__restrict__ img, c
     const long long S = (long long)W * H;
     const uchar4 pc = img[(long long)y * W + x];
     float num = 0.00001f, den = 0.00001f;
+    // unrolled: the gathers of 8 taps are issued before their (in-order) sums
+#pragma unroll 8
     for (int i = 0; i < Tr; ++i) {
         const int qy = clampi(y + i - Rr, 0, H - 1);
         const long long q = (long long)qy * W + x;
@@ -217,6 +219,7 @@ __global__ __launch_bounds__(256) void k_ref_h(const uchar4 *__restrict__ img, c
     const long long row = (long long)y * W;
     const uchar4 pc = img[row + x];
     float num = 0.00001f, den = 0.00001f;
+#pragma unroll 8
     for (int i = 0; i < Tr; ++i) {
         const int qx = clampi(x + i - Rr, 0, W - 1);
         const long long q = row + qx;
