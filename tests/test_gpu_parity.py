@@ -222,9 +222,36 @@ def test_vpass_v10_bit_exact(gpu, oracle, T, H, W, D, d0, d1):
         assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
 
 
-# every compiled pass variant (asw_tune_set): H block shapes, on shapes that hit
-# segment / row edges
-@pytest.mark.parametrize("variant", [0, 64])
+# H pass k_hpass11 (one right-weight LDS ring per block of 4, 2 or 1 plane blocks:
+# Dp = 256, 512 / 128 / 192, 64), every den mode, several segments per row, a shard
+# whose first plane is not 0; T = 33 and the 1-wave blocks refill 4 entries per batch
+@pytest.mark.parametrize("T", [5, 33, 35, 51])
+@pytest.mark.parametrize("H,W,D,d0,d1", [(7, 530, 256, 0, 256), (3, 300, 520, 4, 516), (4, 290, 300, 40, 296),
+                                          (5, 410, 128, 0, 128), (6, 333, 200, 8, 200), (3, 150, 64, 0, 50)])
+def test_hpass_h11_bit_exact(gpu, oracle, T, H, W, D, d0, d1):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    Lh, Rh = _rand_pair(T * 5 + W, H, W, shift=7)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
+    Dp = K.cost_shape(p)[2]
+    rng = np.random.default_rng(T + W)
+    sl, sr = oracle.support(Lh, T, 1), oracle.support(Rh, T, 1)
+    wl, wr = K.asw_hSupport(p, _t(Lh, gpu)), K.asw_hSupport(p, _t(Rh, gpu))
+    den = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+    for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
+        cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+        want = oracle.aggregate_pass(sl, sr, cin, T, 1, d0=d0, d1=d1, plane_base=d0)
+        out = K.asw_hCostAggregation(p, wl, wr, _t(pixel_major(cin, Dp), gpu), den=den, den_mode=mode)
+        got = plane_major(_np(out), d1 - d0)
+        assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
+
+
+# every compiled pass variant (asw_tune_set): H block shapes (64: k_hpass9 with 10
+# waves; 128: k_hpass9 where k_hpass11 would run; 512: k_hpass11 with 2-chunk
+# segments), on shapes that hit segment / row edges
+@pytest.mark.parametrize("variant", [0, 64, 128, 192, 512])
 @pytest.mark.parametrize("H,W,D,d0,d1", [(9, 331, 256, 0, 256), (6, 47, 128, 0, 128), (5, 161, 300, 40, 168),
                                           (4, 400, 256, 128, 256)])
 def test_pass_variants_bit_exact(gpu, oracle, variant, H, W, D, d0, d1):

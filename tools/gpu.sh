@@ -63,7 +63,7 @@ for step in "$@"; do
         prof)
             run 600 "prof_$TAG" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                 python3 bench.py --steps 5 --warmup 1 --no-cpu $args ;;
-        pass) run 600 "pass_$TAG" $PY tools/pass_bench.py --reps 6 --den ${args:---variants 0} ;;
+        pass) run 600 "pass_$TAG${arg:+_${args// /_}}" $PY tools/pass_bench.py --reps 6 --den ${args:---variants 0} ;;
         pmc)
             i=0
             for set in "${PMC_SETS[@]}"; do

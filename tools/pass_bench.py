@@ -34,8 +34,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="0,1,2,3,4,5,8,9")
     ap.add_argument("--den", action="store_true", help="also time the cached-denominator modes (write, read)")
+    ap.add_argument("--ndisp", type=int, default=0, help="override D (e.g. a d-shard's local planes)")
     args = ap.parse_args()
     W, H, D, T, iters, lr, desc = WORKLOADS[args.workload]
+    D = args.ndisp or D
     dev = torch.device("cuda:0")
     Lh, Rh, _ = make_pair(W, H, D, 0)
     p = make_params(W, H, ndisp=D, taps=T, iters=iters)
@@ -74,7 +76,7 @@ def main():
     lib.asw_tune_set(1, 0)
     for (v, d, dm), ts in times.items():
         med = float(np.median(ts))
-        print(json.dumps({"workload": args.workload, "variant": v, "dir": d, "den_mode": dm,
+        print(json.dumps({"workload": args.workload, "ndisp": D, "variant": v, "dir": d, "den_mode": dm,
                           "ms_median": round(med, 4), "ms_min": round(min(ts), 4),
                           "GBps": round(nbytes / med / 1e6, 1),
                           "frac_of_8TBps": round(nbytes / med / 1e6 / 8000, 4)}))
