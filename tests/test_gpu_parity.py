@@ -240,18 +240,22 @@ def test_hpass_h11_bit_exact(gpu, oracle, T, H, W, D, d0, d1):
     sl, sr = oracle.support(Lh, T, 1), oracle.support(Rh, T, 1)
     wl, wr = K.asw_hSupport(p, _t(Lh, gpu)), K.asw_hSupport(p, _t(Rh, gpu))
     den = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
-    for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
-        cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
-        want = oracle.aggregate_pass(sl, sr, cin, T, 1, d0=d0, d1=d1, plane_base=d0)
-        out = K.asw_hCostAggregation(p, wl, wr, _t(pixel_major(cin, Dp), gpu), den=den, den_mode=mode)
-        got = plane_major(_np(out), d1 - d0)
-        assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
+    old = _lib.lib().asw_tune_set(1, 4096)  # k_hpass11 below its frame-size threshold too
+    try:
+        for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
+            cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+            want = oracle.aggregate_pass(sl, sr, cin, T, 1, d0=d0, d1=d1, plane_base=d0)
+            out = K.asw_hCostAggregation(p, wl, wr, _t(pixel_major(cin, Dp), gpu), den=den, den_mode=mode)
+            got = plane_major(_np(out), d1 - d0)
+            assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
+    finally:
+        _lib.lib().asw_tune_set(1, old)
 
 
 # every compiled pass variant (asw_tune_set): H block shapes (64: k_hpass9 with 10
-# waves; 128: k_hpass9 where k_hpass11 would run; 512: k_hpass11 with 2-chunk
+# waves; 128: k_hpass9 always; 4096: k_hpass11 at any size, 512: with 2-chunk
 # segments), on shapes that hit segment / row edges
-@pytest.mark.parametrize("variant", [0, 64, 128, 192, 512])
+@pytest.mark.parametrize("variant", [0, 64, 128, 192, 4096, 4096 + 512])
 @pytest.mark.parametrize("H,W,D,d0,d1", [(9, 331, 256, 0, 256), (6, 47, 128, 0, 128), (5, 161, 300, 40, 168),
                                           (4, 400, 256, 128, 256)])
 def test_pass_variants_bit_exact(gpu, oracle, variant, H, W, D, d0, d1):

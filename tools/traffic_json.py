@@ -25,12 +25,13 @@ DM = {0: "DM_NONE", 1: "DM_WRITE", 2: "DM_READ"}
 
 
 def key_of(name: str):
-    """k_vpass10<35, 16, 2, 2> -> k_vpass10<DM_READ>; k_hpass9<35, 4, 40, 2> -> k_hpass9<DM_READ>."""
-    m = re.match(r"(k_vpass10|k_vpass9|k_hpass9)<([^>]*)>", name)
+    """k_vpass10<35, 16, 2, ...> -> k_vpass10<DM_READ>; k_hpass9<35, 4, 40, 2> -> k_hpass9<DM_READ>;
+    k_hpass11<35, 4, 2, ...> -> k_hpass11<DM_READ> (template argument order of each kernel)."""
+    m = re.match(r"(k_vpass10|k_vpass9|k_hpass9|k_hpass11)<([^>]*)>", name)
     if not m:
         return None
     args = [a.strip() for a in m.group(2).split(",")]
-    dm = int(args[2]) if m.group(1).startswith("k_vpass") else int(args[3])
+    dm = int(args[3]) if m.group(1) == "k_hpass9" else int(args[2])
     return f"{m.group(1)}<{DM[dm]}>"
 
 
