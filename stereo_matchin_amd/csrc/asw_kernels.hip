@@ -125,16 +125,65 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
 // ---------------------------------------------------------------------------
 // asw_vSupport / asw_hSupport (K/asw_vsupport.cl:3-27, K/asw_hsupport.cl:3-28).
 // w[y][x][i] = LUT[|delta|][SAD(p,q)], q the i-th tap of p's 1-D window.
-// One thread = one pixel's group of 4 taps (a float4 store); blockIdx.z selects one
+// One thread = one pixel, lanes = 64 consecutive x of one row: the neighbour of
+// tap i is one coalesced 256-B load per wave (V: row y+i-R; H: the row shifted by
+// i-R), the LUT row of tap i is one dist (except at clamped edges), so its gather
+// stays inside 3 KB of L1.  All Q groups of a pixel are computed before its Q
+// float4 stores (the loads of every tap in flight together); blockIdx.z selects one
 // of up to four (image, direction) jobs, so the four arrays of a frame are one
-// launch with four independent gathers per thread in flight.
+// launch.  (Round 2's float4-per-thread form: 0.67 ms at C4.)
 // ---------------------------------------------------------------------------
 struct SupportJobs {
     const uchar4 *img[4];
     float *w[4];
     int dir[4];
 };
+template <int Q>
 __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *__restrict__ lut, int W, int H,
+                                                 int T) {
+    using f4 = float __attribute__((ext_vector_type(4)));
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    const uchar4 *__restrict__ img = jobs.img[blockIdx.z];
+    const int dir = jobs.dir[blockIdx.z];
+    const int R = T / 2;
+    const uchar4 a = img[y * W + x];
+    f4 *out = reinterpret_cast<f4 *>(jobs.w[blockIdx.z] + ((long long)y * W + x) * (4 * Q));
+    // all 4Q neighbour loads, then all 4Q LUT gathers, in flight together (chunks of
+    // 3 or 5 groups measured 0.86 / 0.61 ms against 0.49 at C4: latency-bound)
+    {
+        constexpr int q0 = 0, NG = Q;
+        uchar4 b[4 * NG];
+#pragma unroll
+        for (int k = 0; k < 4 * NG; ++k) {
+            const int i = 4 * q0 + k;
+            const int qx = dir == ASW_DIR_V ? x : clampi(x + i - R, 0, W - 1);
+            const int qy = dir == ASW_DIR_V ? clampi(y + i - R, 0, H - 1) : y;
+            b[k] = img[qy * W + qx];
+        }
+        f4 v[NG];
+#pragma unroll
+        for (int k = 0; k < 4 * NG; ++k) {
+            const int i = 4 * q0 + k;
+            int dist;
+            if (dir == ASW_DIR_V) {
+                const int qy = clampi(y + i - R, 0, H - 1);
+                dist = y > qy ? y - qy : qy - y;
+            } else {
+                const int qx = clampi(x + i - R, 0, W - 1);
+                dist = x > qx ? x - qx : qx - x;
+            }
+            const int sad = abs((int)a.x - (int)b[k].x) + abs((int)a.y - (int)b[k].y) + abs((int)a.z - (int)b[k].z);
+            v[k / 4][k % 4] = i < T ? lut[dist * kLutWidth + sad] : 0.0f;
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) out[q0 + g] = v[g];
+    }
+}
+
+// any tap count (Q past the unrolled forms): one float4 group per thread
+__global__ __launch_bounds__(256) void k_support_any(SupportJobs jobs, const float *__restrict__ lut, int W, int H,
                                                  int T, int Tp) {
     using f4 = float __attribute__((ext_vector_type(4)));
     const int y = blockIdx.y;
@@ -163,6 +212,13 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
         v[j] = i < T ? lut[dist * kLutWidth + sad] : 0.0f;
     }
     reinterpret_cast<f4 *>(jobs.w[blockIdx.z] + (long long)y * W * Tp)[t] = v;
+}
+
+template <int Q>
+void launch_support_q(const asw_params *p, const SupportJobs &jobs, int njobs, const float *lut,
+                             hipStream_t st) {
+    const dim3 grid((unsigned)((p->width + 63) / 64), (unsigned)((p->height + 3) / 4), (unsigned)njobs);
+    hipLaunchKernelGGL(k_support<Q>, grid, dim3(256), 0, st, jobs, lut, p->width, p->height, p->taps);
 }
 
 // ---------------------------------------------------------------------------
@@ -604,10 +660,23 @@ int asw_support_lut(const asw_params *p, float *lut, void *stream) {
 }
 
 static int launch_support(const asw_params *p, const SupportJobs &jobs, int njobs, const float *lut, void *stream) {
-    const int Tp = asw_tap_pitch(p);
-    const dim3 grid((unsigned)((p->width * (Tp / 4) + 255) / 256), (unsigned)p->height, (unsigned)njobs);
-    hipLaunchKernelGGL(k_support, grid, dim3(256), 0, (hipStream_t)stream, jobs, lut, p->width, p->height, p->taps,
-                       Tp);
+    const hipStream_t st = (hipStream_t)stream;
+    switch (asw_tap_pitch(p) / 4) {  // Tp = 4Q, Q odd past 1 (tap_pitch)
+        case 1: launch_support_q<1>(p, jobs, njobs, lut, st); break;
+        case 3: launch_support_q<3>(p, jobs, njobs, lut, st); break;
+        case 5: launch_support_q<5>(p, jobs, njobs, lut, st); break;
+        case 7: launch_support_q<7>(p, jobs, njobs, lut, st); break;
+        case 9: launch_support_q<9>(p, jobs, njobs, lut, st); break;
+        case 11: launch_support_q<11>(p, jobs, njobs, lut, st); break;
+        case 13: launch_support_q<13>(p, jobs, njobs, lut, st); break;
+        case 15: launch_support_q<15>(p, jobs, njobs, lut, st); break;
+        case 17: launch_support_q<17>(p, jobs, njobs, lut, st); break;
+        default: {
+            const int Tp = asw_tap_pitch(p);
+            const dim3 grid((unsigned)((p->width * (Tp / 4) + 255) / 256), (unsigned)p->height, (unsigned)njobs);
+            hipLaunchKernelGGL(k_support_any, grid, dim3(256), 0, st, jobs, lut, p->width, p->height, p->taps, Tp);
+        }
+    }
     return finish_launch();
 }
 

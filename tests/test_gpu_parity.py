@@ -78,10 +78,16 @@ def test_raw_cost_truncated(gpu, oracle):
     assert np.array_equal(c, np.minimum(oracle.raw_cost(Lh, Rh, 10), np.float32(40.0)))
 
 
-@pytest.mark.parametrize("T", [3, 5, 33, 35, 51])
-def test_support(gpu, oracle, T):
+# T = 71: the generic float4-per-thread kernel (Q = 19 past the unrolled forms);
+# the random pair is ragged (W not a multiple of 64, H of 4)
+@pytest.mark.parametrize("T", [1, 3, 5, 33, 35, 51, 71])
+@pytest.mark.parametrize("scene", ["tsukuba", "ragged"])
+def test_support(gpu, oracle, T, scene):
     import stereo_matchin_amd.kernels as K
-    Lh, Rh, _ = load_scene("tsukuba")
+    if scene == "tsukuba":
+        Lh, Rh, _ = load_scene("tsukuba")
+    else:
+        Lh, Rh = _rand_pair(T, 45, 67)
     p = _params(Lh.shape[1], Lh.shape[0], 16, T)
     Tp = K.support_shape(p)[2]
     for img in (Lh, Rh):
