@@ -29,6 +29,14 @@ constexpr int kTilePitch = kChunk + 1;
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc_n(const void *p, int nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, nbytes, 0x00020000);
+}
+__device__ __forceinline__ float bload(rsrc_t r, int voff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+}
+
 // one element of the sequential scan (K/asw_wta.cl:43-46 order)
 __device__ __forceinline__ void scan_step(float t, int d, float &cur, float &last, int &md) {
     last = t < last ? t : last;
@@ -124,43 +132,61 @@ __global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if (!live) return;
-
-    // target scan (K/asw_wta.cl:50-67, K/asw_wta_ref.cl:39-57)
-    const int x = (int)(p % W), y = (int)(p / W);
+    // target scan (K/asw_wta.cl:50-67, K/asw_wta_ref.cl:39-57): lane l visits
+    // (xq, b) = (max(0, x-i), md + xq - x) for i = 0..md-1, in that order.  The
+    // lanes are skewed: at wave step j lane l is at i = j - (63 - l), so when the
+    // wave's 64 pixels are consecutive in one row every lane reads the SAME
+    // pixel xq = x0 + 63 - j, at planes md_l - i_l that a smooth disparity keeps
+    // within a few cache lines.  An unskewed gather (every lane at the same i)
+    // touches 64 distinct lines per load and is bound by the L1 tag rate.  Each
+    // lane still scans its own i in ascending order, so ties and the multiset
+    // second minimum are those of the sequential loop.
+    const long long pc = live ? p : S - 1;
+    const int x = (int)(pc % W);
+    const int mdl = live ? md : 0;
     float at = 0.0f, valt = 0.0f;
     if constexpr (MODE == 1) {
-        at = 0.085f * ref_r[S + p];
-        valt = ref_r[p];
+        at = 0.085f * ref_r[S + pc];
+        valt = ref_r[pc];
     }
-    const float *crow = cost + (long long)y * W * Dp;
+    int jend = mdl;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) jend = max(jend, __shfl_xor(jend, o));
+    jend += 63;
+    const int skew = 63 - lane;
+    // Buffer addressing from the start of the wave's first row (wave-uniform
+    // base): the element of step i <= x is pixel x-i at plane md-i, one
+    // (Dp+1)-float stride per step, so its byte offset is A - (j+k)*stride with
+    // A per lane and (j+k)*stride uniform; past x it clamps to (0, md-x), the
+    // max() below.  A lane outside its [0, md) window reads a masked value
+    // (out-of-range offsets return 0 through the buffer range check).
+    const long long y0W = p0 / W * W;
+    const long long vol_left = (S - y0W) * Dp * 4;
+    const rsrc_t rsc = make_rsrc_n(cost + y0W * Dp, vol_left < 0x7fffffffLL ? (int)vol_left : 0x7fffffff);
+    const int lanepix = (int)(pc - y0W);
+    const int stride = (Dp + 1) * 4;
+    const int A = (lanepix * Dp + mdl) * 4 + skew * stride;
+    const int flo = ((lanepix - x) * Dp + mdl - x) * 4;
     float cur_t = kSentinel, last_t = kSentinel;
-    int mdr = md;
-    // the diagonal gathers are independent of the scan: issue 8 before consuming
-    // any, so the loop is bound by load throughput rather than one latency per plane
-    int i = 0;
-    for (; i + 8 <= md; i += 8) {
-        float tv[8];
+    int mi = skew;  // the argmin's wave step (i = mi - skew); i = 0 maps back to b = md
+    // kGather steps' gathers are issued before any is consumed
+    constexpr int kGather = 16;
+    for (int j = 0; j < jend; j += kGather) {
+        float tv[kGather];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int xq = x - (i + k) < 0 ? 0 : x - (i + k);
-            tv[k] = crow[(long long)xq * Dp + (md + xq - x)];
-        }
+        for (int k = 0; k < kGather; ++k) tv[k] = bload(rsc, max(A - (j + k) * stride, flo));
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int xq = x - (i + k) < 0 ? 0 : x - (i + k);
+        for (int k = 0; k < kGather; ++k) {
+            const int i = j + k - skew;
             float t = tv[k];
-            if constexpr (MODE == 1) t = penalty(at, valt, i + k, t);
-            scan_step(t, md + xq - x, cur_t, last_t, mdr);
+            if constexpr (MODE == 1) t = penalty(at, valt, i, t);
+            // a value >= the sentinel never changes the scan state: +inf masks
+            t = (unsigned)i < (unsigned)mdl ? t : __builtin_inff();
+            scan_step(t, j + k, cur_t, last_t, mi);
         }
     }
-    for (; i < md; ++i) {
-        const int xq = x - i < 0 ? 0 : x - i;
-        const int b = md + xq - x;
-        float t = crow[(long long)xq * Dp + b];
-        if constexpr (MODE == 1) t = penalty(at, valt, i, t);
-        scan_step(t, b, cur_t, last_t, mdr);
-    }
+    const int mdr = mdl - min(mi - skew, x);  // b = md + max(0, x-i) - x
+    if (!live) return;
     d_ref[p] = md;
     d_tar[p] = mdr;
     if constexpr (MODE == 0) {
