@@ -82,7 +82,7 @@ __global__ void k_support_lut(float *lut, int rows, float gamma_c, float gamma_g
 // planes d = 4q..4q+3 read LDS instead of four gathers; the left pixel is
 // wave-uniform.  Every store is a float4 per lane (1 KB per wave-instruction).
 // ---------------------------------------------------------------------------
-constexpr int kRawPPW = 8;                        // pixels per wave
+constexpr int kRawPPW = 16;                       // pixels per wave
 constexpr int kRawSpan = 4 * kRawPPW;              // pixels per block
 __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, const uchar4 *__restrict__ R,
                                                    float *__restrict__ cost, int W, int Dp, int nloc, int d_begin,
@@ -142,43 +142,58 @@ template <int Q>
 __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *__restrict__ lut, int W, int H,
                                                  int T) {
     using f4 = float __attribute__((ext_vector_type(4)));
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= W || y >= H) return;
+    __shared__ f4 stg[4][64 * Q];  // per wave: its 64 pixels' Q float4, in output order
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int x0 = blockIdx.x * 64;
+    const int y = blockIdx.y * 4 + wv;
+    if (y >= H) return;  // whole wave
+    const int x = min(x0 + lane, W - 1);  // lanes past the right edge recompute column W-1, not stored
     const uchar4 *__restrict__ img = jobs.img[blockIdx.z];
     const int dir = jobs.dir[blockIdx.z];
     const int R = T / 2;
     const uchar4 a = img[y * W + x];
-    f4 *out = reinterpret_cast<f4 *>(jobs.w[blockIdx.z] + ((long long)y * W + x) * (4 * Q));
     // all 4Q neighbour loads, then all 4Q LUT gathers, in flight together (chunks of
     // 3 or 5 groups measured 0.86 / 0.61 ms against 0.49 at C4: latency-bound)
     {
-        constexpr int q0 = 0, NG = Q;
+        constexpr int NG = Q;
         uchar4 b[4 * NG];
 #pragma unroll
         for (int k = 0; k < 4 * NG; ++k) {
-            const int i = 4 * q0 + k;
-            const int qx = dir == ASW_DIR_V ? x : clampi(x + i - R, 0, W - 1);
-            const int qy = dir == ASW_DIR_V ? clampi(y + i - R, 0, H - 1) : y;
+            const int qx = dir == ASW_DIR_V ? x : clampi(x + k - R, 0, W - 1);
+            const int qy = dir == ASW_DIR_V ? clampi(y + k - R, 0, H - 1) : y;
             b[k] = img[qy * W + qx];
         }
         f4 v[NG];
 #pragma unroll
         for (int k = 0; k < 4 * NG; ++k) {
-            const int i = 4 * q0 + k;
             int dist;
             if (dir == ASW_DIR_V) {
-                const int qy = clampi(y + i - R, 0, H - 1);
+                const int qy = clampi(y + k - R, 0, H - 1);
                 dist = y > qy ? y - qy : qy - y;
             } else {
-                const int qx = clampi(x + i - R, 0, W - 1);
+                const int qx = clampi(x + k - R, 0, W - 1);
                 dist = x > qx ? x - qx : qx - x;
             }
             const int sad = abs((int)a.x - (int)b[k].x) + abs((int)a.y - (int)b[k].y) + abs((int)a.z - (int)b[k].z);
-            v[k / 4][k % 4] = i < T ? lut[dist * kLutWidth + sad] : 0.0f;
+            v[k / 4][k % 4] = k < T ? lut[dist * kLutWidth + sad] : 0.0f;
         }
+        // The wave's 64 pixels are one contiguous 64*Q-float4 run of the output:
+        // transposed through LDS (Q odd: the 144-B lane stride of the writes is
+        // bank-conflict-free), every store is then one coalesced 1-KB wave access
+        // instead of 64 float4 at a 16Q-byte stride.
+        f4 *st = stg[wv];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) out[q0 + g] = v[g];
+        for (int g = 0; g < NG; ++g) st[lane * Q + g] = v[g];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int nval = min(64, W - x0) * Q;
+        f4 *out = reinterpret_cast<f4 *>(jobs.w[blockIdx.z] + ((long long)y * W + x0) * (4 * Q));
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int e = g * 64 + lane;
+            if (e < nval) out[e] = st[e];
+        }
     }
 }
 
