@@ -46,6 +46,11 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
 int set_pass_variant(int v);
 
 // lane-per-pixel WTA scan (asw_refine.hip): mode 0 = asw_WTA, 1 = asw_WTA_REF
+// lane-per-pixel d-sharded WTA halves (ref = NULL: asw_WTA; else asw_WTA_REF's penalty)
+int launch_wta_local_scan(const asw_params *p, const float *cost, const float *ref, long long *key, float *m1,
+                          float *m2, hipStream_t st);
+int launch_wta_target_local_scan(const asw_params *p, const float *cost, const long long *key_ref, const float *ref,
+                                 long long *tkey, float *t1, float *t2, hipStream_t st);
 int launch_wta_scan(const asw_params *p, int mode, const float *cost, const float *ref_l, const float *ref_r,
                     int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar, uint8_t *code_ref,
                     uint8_t *code_tar, hipStream_t st);

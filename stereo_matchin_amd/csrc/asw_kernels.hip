@@ -103,10 +103,13 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
     const int nq = Dp >> 2;
     const int xa = x0 + wave * kRawPPW;
     const int xb = min(xa + kRawPPW, W);
-    for (int x = xa; x < xb; ++x) {
+    // Dp < 256 (narrow shards): 64/nq pixels per wave iteration, so no lane idles
+    const int ppi = (nq < 64 && 64 % nq == 0) ? 64 / nq : 1;
+    const int lpp = ppi > 1 ? nq : 64;  // lanes per pixel
+    for (int x = xa + lane / lpp; x < xb; x += ppi) {
         const uchar4 l = Lrow[x];
         f4 *out = reinterpret_cast<f4 *>(cost + ((long long)y * W + x) * Dp);
-        for (int q = lane; q < nq; q += 64) {
+        for (int q = lane % lpp; q < nq; q += lpp) {
             f4 v;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -808,6 +811,9 @@ int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_
 int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m1, float *m2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !key || !m1 || !m2) return ASW_E_INVALID;
+    if (g_wta_variant == 0)
+        return asw::launch_wta_local_scan(p, cost, nullptr, reinterpret_cast<long long *>(key), m1, m2,
+                                          (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
     const int bpx = (int)(((n + 3) / 4 + 7) / 8);
     hipLaunchKernelGGL(k_wta_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
@@ -820,6 +826,9 @@ int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *
                          float *t2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
+    if (g_wta_variant == 0)
+        return asw::launch_wta_target_local_scan(p, cost, reinterpret_cast<const long long *>(key_ref), nullptr,
+                                                 reinterpret_cast<long long *>(tkey), t1, t2, (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
     const int bpx = (int)(((n + 3) / 4 + 7) / 8);
     hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
@@ -833,6 +842,9 @@ int asw_wta_ref_local(const asw_params *p, const float *cost, const float *ref_l
                       void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !ref_l || !key || !m1 || !m2) return ASW_E_INVALID;
+    if (g_wta_variant == 0)
+        return asw::launch_wta_local_scan(p, cost, ref_l, reinterpret_cast<long long *>(key), m1, m2,
+                                          (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
     const int bpx = (int)(((n + 3) / 4 + 7) / 8);
     hipLaunchKernelGGL(k_wta_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
@@ -845,6 +857,9 @@ int asw_wta_ref_target_local(const asw_params *p, const float *cost, const float
                              int64_t *tkey, float *t1, float *t2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !ref_r || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
+    if (g_wta_variant == 0)
+        return asw::launch_wta_target_local_scan(p, cost, reinterpret_cast<const long long *>(key_ref), ref_r,
+                                                 reinterpret_cast<long long *>(tkey), t1, t2, (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
     const int bpx = (int)(((n + 3) / 4 + 7) / 8);
     hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,

@@ -56,28 +56,13 @@ __device__ __forceinline__ float penalty(float a, float val, int i, float c) {
 //   estimates ref_l / ref_r ([2][S]: value plane, den plane); outputs d_ref,
 //   d_tar, codes, and conf_ref <- the TARGET confidence (the kernel's second,
 //   overwriting store to `confidence`, K/asw_wta_ref.cl:64-66); conf_tar untouched.
-template <int MODE>
-__global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost, int W, int H, int Dp, int D,
-                                                  const float *__restrict__ ref_l, const float *__restrict__ ref_r,
-                                                  int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
-                                                  int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
-                                                  uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar,
-                                                  int nwaves, int per_xcd) {
+// Own scan of the wave's 64 pixels over `nplanes` planes of a pixel-major volume
+// (pitch Dp): the scanned index and the penalty's i are dbase + k.
+template <bool PEN>
+__device__ __forceinline__ void own_scan(float *tile, const float *__restrict__ cost, long long p0, long long S, int Dp,
+                                         int nplanes, int dbase, int lane, float a, float val, float &cur, float &last,
+                                         int &md) {
     using f4 = float __attribute__((ext_vector_type(4)));
-    __shared__ float tile_all[4][64 * kTilePitch];
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    // XCD-aware: blocks b, b+8, b+16, ... run on one XCD; give each XCD a
-    // contiguous range of per_xcd blocks (4 waves each) so its target gathers hit
-    // rows its L2 just streamed
-    const int wave_id = ((blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3)) * 4 + wv;
-    if (wave_id >= nwaves) return;
-    float *tile = tile_all[wv];
-    const long long S = (long long)W * H;
-    const long long p0 = (long long)wave_id * 64;
-    const long long p = p0 + lane;
-    const bool live = p < S;
-
     // chunk loader: instruction j (0..7) of lane l covers pixel j*8 + l/8, planes (l%8)*4..+3
     const int sub = lane & 7, prow = lane >> 3;
     const float *src[8];
@@ -87,18 +72,9 @@ __global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost
         src[j] = cost + pp * Dp + sub * 4;
     }
     f4 buf[8];
-    const int nchunk = (D + kChunk - 1) / kChunk;
+    const int nchunk = (nplanes + kChunk - 1) / kChunk;
 #pragma unroll
     for (int j = 0; j < 8; ++j) buf[j] = *reinterpret_cast<const f4 *>(src[j]);
-
-    float a = 0.0f, val = 0.0f;
-    if constexpr (MODE == 1) {
-        const long long pq = live ? p : S - 1;
-        a = 0.085f * ref_l[S + pq];
-        val = ref_l[pq];
-    }
-    float cur = kSentinel, last = kSentinel;
-    int md = 0;
     for (int c = 0; c < nchunk; ++c) {
         // transpose the chunk into the wave's tile (row = pixel)
 #pragma unroll
@@ -116,62 +92,78 @@ __global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost
         __builtin_amdgcn_wave_barrier();
         const float *mine = tile + lane * kTilePitch;
         const int d0 = c * kChunk;
-        if (d0 + kChunk <= D) {
+        if (d0 + kChunk <= nplanes) {
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
                 float t = mine[k];
-                if constexpr (MODE == 1) t = penalty(a, val, d0 + k, t);
-                scan_step(t, d0 + k, cur, last, md);
+                if constexpr (PEN) t = penalty(a, val, dbase + d0 + k, t);
+                scan_step(t, dbase + d0 + k, cur, last, md);
             }
         } else {
-            for (int k = 0; k < D - d0; ++k) {
+            for (int k = 0; k < nplanes - d0; ++k) {
                 float t = mine[k];
-                if constexpr (MODE == 1) t = penalty(a, val, d0 + k, t);
-                scan_step(t, d0 + k, cur, last, md);
+                if constexpr (PEN) t = penalty(a, val, dbase + d0 + k, t);
+                scan_step(t, dbase + d0 + k, cur, last, md);
             }
         }
         __builtin_amdgcn_wave_barrier();
     }
-    // target scan (K/asw_wta.cl:50-67, K/asw_wta_ref.cl:39-57): lane l visits
-    // (xq, b) = (max(0, x-i), md + xq - x) for i = 0..md-1, in that order.  The
-    // lanes are skewed: at wave step j lane l is at i = j - (63 - l), so when the
-    // wave's 64 pixels are consecutive in one row every lane reads the SAME
-    // pixel xq = x0 + 63 - j, at planes md_l - i_l that a smooth disparity keeps
-    // within a few cache lines.  An unskewed gather (every lane at the same i)
-    // touches 64 distinct lines per load and is bound by the L1 tag rate.  Each
-    // lane still scans its own i in ascending order, so ties and the multiset
-    // second minimum are those of the sequential loop.
-    const long long pc = live ? p : S - 1;
-    const int x = (int)(pc % W);
-    const int mdl = live ? md : 0;
-    float at = 0.0f, valt = 0.0f;
-    if constexpr (MODE == 1) {
-        at = 0.085f * ref_r[S + pc];
-        valt = ref_r[pc];
-    }
-    int jend = mdl;
+}
+
+__device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) jend = max(jend, __shfl_xor(jend, o));
-    jend += 63;
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Target scan (K/asw_wta.cl:50-67, K/asw_wta_ref.cl:39-57) of pixel pc (x) with
+// left disparity md: for i = 0..md-1, xq = max(0, x-i), b = md + xq - x, value
+// C[b][y][xq].  Only b in [b_lo, b_lo + nloc) (this volume's planes; local plane
+// b - b_lo) is visited: b = md - min(i, x) is non-increasing in i, so that is one
+// interval [i_lo, i_hi) of i.
+//   The lanes are skewed: at wave step j lane l is at i = j - (63 - l), so when
+// the wave's 64 pixels are consecutive in one row every lane reads the SAME pixel
+// xq = x0 + 63 - j, at planes md_l - i_l that a smooth disparity keeps within a
+// few cache lines (an unskewed gather touches 64 distinct lines per load and is
+// bound by the L1 tag rate).  Each lane still scans its own i in ascending order,
+// so ties and the multiset second minimum are the sequential loop's.
+//   Buffer addressing from the start of the wave's first row (wave-uniform base):
+// the element of step i <= x is pixel x-i at plane md-i, one (Dp+1)-float stride
+// per step, so its byte offset is A - (j+k)*stride with A per lane and
+// (j+k)*stride uniform; past x it clamps to (0, md-x), the max() below.  A lane
+// outside its interval reads a masked value (out-of-range offsets return 0
+// through the buffer range check).  ibest = the first argmin's i, -1 if none.
+template <bool PEN>
+__device__ __forceinline__ void target_scan_skewed(const float *__restrict__ cost, long long p0, long long pc,
+                                                   long long S, int W, int Dp, int md, int b_lo, int nloc, int lane,
+                                                   float at, float valt, float &cur_t, float &last_t, int &ibest) {
+    const int x = (int)(pc % W);
+    const int b_hi = b_lo + nloc;
+    int i_lo = max(0, md - b_hi + 1), i_hi = x <= md - b_lo ? md : min(md, md - b_lo + 1);
+    if (x <= md - b_hi) i_hi = 0;  // every b(i) >= b_hi
     const int skew = 63 - lane;
-    // Buffer addressing from the start of the wave's first row (wave-uniform
-    // base): the element of step i <= x is pixel x-i at plane md-i, one
-    // (Dp+1)-float stride per step, so its byte offset is A - (j+k)*stride with
-    // A per lane and (j+k)*stride uniform; past x it clamps to (0, md-x), the
-    // max() below.  A lane outside its [0, md) window reads a masked value
-    // (out-of-range offsets return 0 through the buffer range check).
+    const bool any = i_lo < i_hi;
+    const int jbeg = wave_min(any ? i_lo + skew : 0x7fffffff);
+    const int jend = wave_max(any ? i_hi + skew : -1);
+    const int ilen = any ? i_hi - i_lo : 0;
     const long long y0W = p0 / W * W;
     const long long vol_left = (S - y0W) * Dp * 4;
     const rsrc_t rsc = make_rsrc_n(cost + y0W * Dp, vol_left < 0x7fffffffLL ? (int)vol_left : 0x7fffffff);
     const int lanepix = (int)(pc - y0W);
     const int stride = (Dp + 1) * 4;
-    const int A = (lanepix * Dp + mdl) * 4 + skew * stride;
-    const int flo = ((lanepix - x) * Dp + mdl - x) * 4;
-    float cur_t = kSentinel, last_t = kSentinel;
-    int mi = skew;  // the argmin's wave step (i = mi - skew); i = 0 maps back to b = md
+    const int A = (lanepix * Dp + md - b_lo) * 4 + skew * stride;
+    const int flo = ((lanepix - x) * Dp + md - x - b_lo) * 4;
+    cur_t = kSentinel;
+    last_t = kSentinel;
+    int mi = -1;  // the argmin's wave step j+k (i = mi - skew)
     // kGather steps' gathers are issued before any is consumed
     constexpr int kGather = 16;
-    for (int j = 0; j < jend; j += kGather) {
+    for (int j = jbeg; j < jend; j += kGather) {
         float tv[kGather];
 #pragma unroll
         for (int k = 0; k < kGather; ++k) tv[k] = bload(rsc, max(A - (j + k) * stride, flo));
@@ -179,13 +171,55 @@ __global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost
         for (int k = 0; k < kGather; ++k) {
             const int i = j + k - skew;
             float t = tv[k];
-            if constexpr (MODE == 1) t = penalty(at, valt, i, t);
+            if constexpr (PEN) t = penalty(at, valt, i, t);
             // a value >= the sentinel never changes the scan state: +inf masks
-            t = (unsigned)i < (unsigned)mdl ? t : __builtin_inff();
+            t = (unsigned)(i - i_lo) < (unsigned)ilen ? t : __builtin_inff();
             scan_step(t, j + k, cur_t, last_t, mi);
         }
     }
-    const int mdr = mdl - min(mi - skew, x);  // b = md + max(0, x-i) - x
+    ibest = mi < 0 ? -1 : mi - skew;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost, int W, int H, int Dp, int D,
+                                                  const float *__restrict__ ref_l, const float *__restrict__ ref_r,
+                                                  int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
+                                                  int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
+                                                  uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar,
+                                                  int nwaves, int per_xcd) {
+    __shared__ float tile_all[4][64 * kTilePitch];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    // XCD-aware: blocks b, b+8, b+16, ... run on one XCD; give each XCD a
+    // contiguous range of per_xcd blocks (4 waves each) so its target gathers hit
+    // rows its L2 just streamed
+    const int wave_id = ((blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3)) * 4 + wv;
+    if (wave_id >= nwaves) return;
+    const long long S = (long long)W * H;
+    const long long p0 = (long long)wave_id * 64;
+    const long long p = p0 + lane;
+    const bool live = p < S;
+    const long long pc = live ? p : S - 1;
+
+    float a = 0.0f, val = 0.0f;
+    if constexpr (MODE == 1) {
+        a = 0.085f * ref_l[S + pc];
+        val = ref_l[pc];
+    }
+    float cur = kSentinel, last = kSentinel;
+    int md = 0;
+    own_scan<MODE == 1>(tile_all[wv], cost, p0, S, Dp, D, 0, lane, a, val, cur, last, md);
+
+    float at = 0.0f, valt = 0.0f;
+    if constexpr (MODE == 1) {
+        at = 0.085f * ref_r[S + pc];
+        valt = ref_r[pc];
+    }
+    float cur_t, last_t;
+    int ib;
+    target_scan_skewed<MODE == 1>(cost, p0, pc, S, W, Dp, live ? md : 0, 0, D, lane, at, valt, cur_t, last_t, ib);
+    const int x = (int)(pc % W);
+    const int mdr = ib < 0 ? md : md - min(ib, x);  // b = md + max(0, x-i) - x
     if (!live) return;
     d_ref[p] = md;
     d_tar[p] = mdr;
@@ -197,6 +231,76 @@ __global__ __launch_bounds__(256) void k_wta_scan(const float *__restrict__ cost
     }
     if (code_ref) code_ref[p] = (uint8_t)code_u8(md, D);
     if (code_tar) code_tar[p] = (uint8_t)code_u8(mdr, D);
+}
+
+__device__ __forceinline__ long long scan_key(float v, int idx) {
+    return (long long)(((unsigned long long)__float_as_uint(v) << 32) | (unsigned)idx);
+}
+constexpr long long kNoKeyScan = 0x7fffffffffffffffLL;
+
+// d-sharded WTA, lane per pixel: the local halves of asw_wta_local /
+// asw_wta_ref_local (own scan of planes [d_begin, d_begin + nloc): key =
+// (m1 bits << 32 | first argmin), m1, m2) ...
+template <bool PEN>
+__global__ __launch_bounds__(256) void k_wta_local_scan(const float *__restrict__ cost, int W, int H, int Dp,
+                                                        int d_begin, int nloc, const float *__restrict__ ref,
+                                                        long long *__restrict__ key, float *__restrict__ m1,
+                                                        float *__restrict__ m2, int nwaves, int per_xcd) {
+    __shared__ float tile_all[4][64 * kTilePitch];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int wave_id = ((blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3)) * 4 + wv;
+    if (wave_id >= nwaves) return;
+    const long long S = (long long)W * H;
+    const long long p0 = (long long)wave_id * 64;
+    const long long p = p0 + lane;
+    const long long pc = p < S ? p : S - 1;
+    float a = 0.0f, val = 0.0f;
+    if constexpr (PEN) {
+        a = 0.085f * ref[S + pc];
+        val = ref[pc];
+    }
+    float cur = kSentinel, last = kSentinel;
+    int md = -1;
+    own_scan<PEN>(tile_all[wv], cost, p0, S, Dp, nloc, d_begin, lane, a, val, cur, last, md);
+    if (p >= S) return;
+    key[p] = md < 0 ? kNoKeyScan : scan_key(cur, md);
+    m1[p] = cur;
+    m2[p] = last;
+}
+
+// ... and of asw_wta_target_local / asw_wta_ref_target_local (the target scan
+// restricted to the local planes, md from the global key; tkey = (t1 bits << 32 | i)).
+template <bool PEN>
+__global__ __launch_bounds__(256) void k_wta_target_local_scan(const float *__restrict__ cost, int W, int H, int Dp,
+                                                               int d_begin, int nloc,
+                                                               const long long *__restrict__ key_ref,
+                                                               const float *__restrict__ ref,
+                                                               long long *__restrict__ tkey, float *__restrict__ t1,
+                                                               float *__restrict__ t2, int nwaves, int per_xcd) {
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int wave_id = ((blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3)) * 4 + wv;
+    if (wave_id >= nwaves) return;
+    const long long S = (long long)W * H;
+    const long long p0 = (long long)wave_id * 64;
+    const long long p = p0 + lane;
+    const bool live = p < S;
+    const long long pc = live ? p : S - 1;
+    const long long kr = key_ref[pc];
+    const int md = (!live || kr == kNoKeyScan) ? 0 : (int)(unsigned)(kr & 0xffffffffLL);
+    float at = 0.0f, valt = 0.0f;
+    if constexpr (PEN) {
+        at = 0.085f * ref[S + pc];
+        valt = ref[pc];
+    }
+    float cur_t, last_t;
+    int ib;
+    target_scan_skewed<PEN>(cost, p0, pc, S, W, Dp, md, d_begin, nloc, lane, at, valt, cur_t, last_t, ib);
+    if (!live) return;
+    tkey[p] = ib < 0 ? kNoKeyScan : scan_key(cur_t, ib);
+    t1[p] = cur_t;
+    t2[p] = last_t;
 }
 
 // asw_ref_v (K/asw_refinement_v.cl:13-51): per pixel, over the Tr vertical taps
@@ -306,6 +410,45 @@ inline int finish() {
 inline int d_end_of(const asw_params *p) { return p->d_end < 0 ? p->ndisp : p->d_end; }
 
 }  // namespace
+
+namespace {
+inline void scan_grid(const asw_params *p, int &nwaves, int &per_xcd, unsigned &nblocks) {
+    const long long S = (long long)p->width * p->height;
+    nwaves = (int)((S + 63) / 64);
+    per_xcd = ((nwaves + 3) / 4 + 7) / 8;  // blocks of 4 waves per XCD, the grid is exactly 8 x per_xcd
+    nblocks = 8u * (unsigned)per_xcd;
+}
+}  // namespace
+
+int launch_wta_local_scan(const asw_params *p, const float *cost, const float *ref, long long *key, float *m1,
+                          float *m2, hipStream_t st) {
+    int nwaves, per_xcd;
+    unsigned nb;
+    scan_grid(p, nwaves, per_xcd, nb);
+    const int Dp = asw_disp_pitch(p), nloc = d_end_of(p) - p->d_begin;
+    if (ref)
+        hipLaunchKernelGGL(k_wta_local_scan<true>, dim3(nb), dim3(256), 0, st, cost, p->width, p->height, Dp,
+                           p->d_begin, nloc, ref, key, m1, m2, nwaves, per_xcd);
+    else
+        hipLaunchKernelGGL(k_wta_local_scan<false>, dim3(nb), dim3(256), 0, st, cost, p->width, p->height, Dp,
+                           p->d_begin, nloc, ref, key, m1, m2, nwaves, per_xcd);
+    return finish();
+}
+
+int launch_wta_target_local_scan(const asw_params *p, const float *cost, const long long *key_ref, const float *ref,
+                                 long long *tkey, float *t1, float *t2, hipStream_t st) {
+    int nwaves, per_xcd;
+    unsigned nb;
+    scan_grid(p, nwaves, per_xcd, nb);
+    const int Dp = asw_disp_pitch(p), nloc = d_end_of(p) - p->d_begin;
+    if (ref)
+        hipLaunchKernelGGL(k_wta_target_local_scan<true>, dim3(nb), dim3(256), 0, st, cost, p->width, p->height, Dp,
+                           p->d_begin, nloc, key_ref, ref, tkey, t1, t2, nwaves, per_xcd);
+    else
+        hipLaunchKernelGGL(k_wta_target_local_scan<false>, dim3(nb), dim3(256), 0, st, cost, p->width, p->height, Dp,
+                           p->d_begin, nloc, key_ref, ref, tkey, t1, t2, nwaves, per_xcd);
+    return finish();
+}
 
 int launch_wta_scan(const asw_params *p, int mode, const float *cost, const float *ref_l, const float *ref_r,
                     int32_t *d_ref, float *conf_ref, int32_t *d_tar, float *conf_tar, uint8_t *code_ref,

@@ -1,0 +1,45 @@
+"""One rank's share of a d-sharded C4 frame on one GPU (no collective: the MIN
+all-reduces are identities without torch.distributed), for rocprofv3 kernel stats
+of the sharded WTA kernels and the replicated side kernels.
+
+    python tools/shard_frame_bench.py [--world 4] [--rank 1] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from stereo_matchin_amd import make_params  # noqa: E402
+from stereo_matchin_amd.distributed import ShardedStereoMatcher  # noqa: E402
+from stereo_matchin_amd.synthetic import make_pair  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=4)
+    ap.add_argument("--rank", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    W, H, D, T, r = 1920, 1080, 256, 35, 7
+    Lh, Rh, _ = make_pair(W, H, D, 0)
+    L, R = torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev)
+    p = make_params(W, H, ndisp=D, taps=T, iters=r, lr_check=1)
+    m = ShardedStereoMatcher(p, a.rank, a.world, dev)
+    m.match(L, R)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        m.match(L, R)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / a.reps
+    print(json.dumps({"world": a.world, "rank": a.rank, "planes": m.p.d_stop - m.p.d_begin,
+                      "ms_per_shard_frame_no_collective": round(ms, 3)}))
+
+
+if __name__ == "__main__":
+    main()
