@@ -21,6 +21,10 @@ int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr
 }
 }  // namespace agg
 
+// any other odd tap count (asw_aggregate_any.hip)
+int launch_pass_any(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                    float *den, int dm, hipStream_t st);
+
 int set_pass_variant(int v) {
     const int old = agg::g_pass_variant;
     agg::g_pass_variant = v;
@@ -35,9 +39,10 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
     const long long rowbytes = (long long)p->width * asw_disp_pitch(p) * 4;
     if (rowbytes * (2LL * p->taps + 16) >= (1LL << 31)) return ASW_E_UNSUPPORTED;
     if ((long long)asw_support_bytes(p) >= (1LL << 31)) return ASW_E_UNSUPPORTED;
-#ifdef ASW_DEV_TAPS  // development build (make DEV=1): one tap count only
-    if (p->taps != ASW_DEV_TAPS) return ASW_E_UNSUPPORTED;
-    return agg::launch_pass_t<ASW_DEV_TAPS>(p, dir, wl, wr, cin, cout, den, dm, st, raw);
+#ifdef ASW_DEV_TAPS  // development build (make DEV=1): one ring-kernel tap count only
+    if (p->taps == ASW_DEV_TAPS) return agg::launch_pass_t<ASW_DEV_TAPS>(p, dir, wl, wr, cin, cout, den, dm, st, raw);
+    if (raw) return ASW_E_UNSUPPORTED;
+    return launch_pass_any(p, dir, wl, wr, cin, cout, den, dm, st);
 #endif
     switch (p->taps) {
 #define ASW_CASE(TT) \
@@ -52,8 +57,9 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
         ASW_CASE(35)
         ASW_CASE(51)
 #undef ASW_CASE
-        default:
-            return ASW_E_UNSUPPORTED;
+        default:  // no ring kernel for this T: the generic pass (the fused raw cost is opt-in, ring kernels only)
+            if (raw) return ASW_E_UNSUPPORTED;
+            return launch_pass_any(p, dir, wl, wr, cin, cout, den, dm, st);
     }
 }
 

@@ -104,7 +104,8 @@ def test_support(gpu, oracle, T, scene):
         assert np.array_equal(np.transpose(_np(w)[:, :, :T], (2, 0, 1)), oracle.support(img, T, direction))
 
 
-@pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35, 51])
+# 1, 11, 21, 37: no ring kernel, the generic pass (asw_aggregate_any.hip)
+@pytest.mark.parametrize("T", [1, 3, 5, 7, 9, 11, 15, 21, 33, 35, 37, 51])
 @pytest.mark.parametrize("direction", [0, 1])
 def test_single_pass_bit_exact(gpu, oracle, T, direction):
     import stereo_matchin_amd.kernels as K
@@ -145,7 +146,7 @@ def test_single_pass_sharded_planes(gpu, oracle, direction):
 
 # cached denominators: a DEN_WRITE pass on one cost volume, then a DEN_READ pass on
 # another with the same supports, each bit-exact against the oracle's full pass
-@pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35, 51])
+@pytest.mark.parametrize("T", [3, 5, 7, 9, 11, 15, 33, 35, 51])
 @pytest.mark.parametrize("direction", [0, 1])
 @pytest.mark.parametrize("H,W,D,d0,d1", [(37, 91, 70, 0, 70), (23, 150, 200, 70, 135)])
 def test_den_cache_write_then_read(gpu, oracle, T, direction, H, W, D, d0, d1):
@@ -361,7 +362,8 @@ def test_e2e_device_png_agreement(gpu, oracle, scene):
 
 @pytest.mark.parametrize("H,W,D,T,iters", [
     (1, 1, 1, 3, 1), (1, 1, 4, 5, 2), (2, 3, 5, 9, 2), (7, 5, 12, 33, 1), (5, 70, 3, 51, 1),
-    (33, 2, 7, 35, 2), (17, 19, 65, 15, 1), (9, 130, 129, 7, 2), (31, 47, 64, 35, 0)])
+    (33, 2, 7, 35, 2), (17, 19, 65, 15, 1), (9, 130, 129, 7, 2), (31, 47, 64, 35, 0),
+    (24, 61, 40, 11, 2), (20, 90, 70, 25, 2)])
 def test_e2e_edge_shapes(gpu, oracle, H, W, D, T, iters):
     Lh, Rh = _rand_pair(H * 1000 + W * 10 + D, H, W, shift=min(3, W - 1))
     _, res = _run(gpu, Lh, Rh, D, T, iters)
