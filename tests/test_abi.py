@@ -1,8 +1,11 @@
 """The C-ABI library loads and exports every symbol include/asw.h declares (CPU only:
 host-side helpers are called, no kernel is launched)."""
 import ctypes
+import os
 
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -119,3 +122,22 @@ def test_frame_api_validates_before_allocating(L):
     assert lib.asw_ctx_shard(None, 0, None, None, None) == L.ASW_E_INVALID
     assert lib.asw_match_batch(None, None, None, 1, None, None) == L.ASW_E_INVALID
     assert L.strerror(L.ASW_E_COMM)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: without libasw_hip.so every product entry point raises
+    AswLibraryError (checked in a child process, ASW_LIB pointing nowhere)."""
+    import subprocess
+    import sys
+    code = (
+        "import torch\n"
+        "from stereo_matchin_amd import _lib, make_params, StereoMatcher\n"
+        "try:\n"
+        "    StereoMatcher(make_params(16, 8, ndisp=4, taps=3, iters=1), torch.device('cpu'))\n"
+        "    _lib.lib()\n"
+        "except _lib.AswLibraryError as e:\n"
+        "    print('LOUD', e)\n"
+    )
+    env = dict(os.environ, ASW_LIB=str(tmp_path / "absent.so"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert "LOUD" in r.stdout, (r.stdout, r.stderr[-2000:])
