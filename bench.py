@@ -137,6 +137,18 @@ def cpu_baseline(Lh, Rh, D, T, iters, rows, lr_mode):
     }
 
 
+def h_kernel_name(W, H, nloc, T):
+    """The H pass kernel launch_dm (asw_aggregate_impl.h) selects for this shape: k_hpass11
+    when its row-segment grid has >= 8192 waves, else k_hpass9."""
+    U = T + 3
+    while U % 4:
+        U += 1
+    seg = (240 + U // 2) // U * U
+    nkb = (nloc + 63) // 64
+    waves = H * ((W + seg - 1) // seg) * nkb
+    return "k_hpass11<DM_READ>" if waves >= 8192 else "k_hpass9<DM_READ>"
+
+
 def load_traffic(path, workload, n_gpus, kernel):
     """Per-launch HBM bytes of `kernel` from profiles/traffic.json (rocprofv3 PMC)."""
     try:
@@ -316,7 +328,7 @@ def main():
         maps_per_s = n_maps / (span_sum / 1e3) if frame else n_maps / elapsed
         dom = "v" if (v_avg >= h_avg or h_avg != h_avg) else "h"
         dom_ms = v_avg if dom == "v" else h_avg
-        kname = "k_vpass10<DM_READ>" if dom == "v" else "k_hpass9<DM_READ>"
+        kname = "k_vpass10<DM_READ>" if dom == "v" else h_kernel_name(W, H, nloc, T)
         out = {
             "metric": METRIC,
             "value": round(maps_per_s, 4),

@@ -71,6 +71,12 @@ void asw_params_default(asw_params *p);
 int asw_params_check(const asw_params *p);
 const char *asw_strerror(int status);
 int asw_last_hip_error(void); /* hipError_t of the last ASW_E_HIP */
+/* ABI revision of this header.  The frame API's caller-allocated structs
+ * (asw_outputs, asw_timings) grow between revisions: a host must check
+ * asw_abi_version() == ASW_ABI_VERSION before calling asw_match / asw_match_batch,
+ * or the library writes past a struct of an older layout.
+ *   1: round 1;  2: asw_outputs.disp16 / lr16, asw_timings.exchange. */
+#define ASW_ABI_VERSION 2
 int asw_abi_version(void);
 
 /* layout helpers */
@@ -251,6 +257,11 @@ int asw_refine(const asw_params *p, const asw_refine_params *rp, const uint8_t *
 #define ASW_TUNE_PASS_VARIANT 1
 #define ASW_TUNE_WTA_VARIANT 2 /* 0: lane-per-pixel scan (default), 1: wave-per-pixel reduction */
 int asw_tune_set(int key, int value);
+/* the kernel instantiation the most recent aggregation-pass launch of (dir, den_mode)
+ * in this process ran, e.g. "k_vpass10<T=35,NW=16,DM=2,nt>" (NUL-terminated, at most
+ * len bytes): lets a test assert which compiled form a shape selects.  ASW_E_INVALID
+ * when no such pass has been launched yet. */
+int asw_pass_kernel(int dir, int den_mode, char *buf, int len);
 
 /* ---------------- FRAME API (host pointers, synchronous) ---------------- */
 
@@ -287,7 +298,9 @@ int asw_device_name(int hip_device, char *buf, int len);
 /* A context owns the device buffers of one image size, sized at create and reused
  * by every asw_match (the reference re-creates its cl_mem objects per run,
  * main.cpp:243-457).  p->d_begin / d_end must cover the whole range: contexts
- * shard the disparity axis themselves.
+ * shard the disparity axis themselves.  Shapes whose volume rows or support arrays
+ * exceed the pass kernels' 32-bit offsets (e.g. 7680x4320 at D = 512) are rejected
+ * here with ASW_E_UNSUPPORTED, before anything is allocated.
  *
  * asw_create: one GPU (HIP device ordinal), the whole disparity range. */
 int asw_create(const asw_params *p, int hip_device, asw_ctx **out);
@@ -306,7 +319,12 @@ int asw_create_multi(const asw_params *p, const int *hip_device_ids, int n_devic
  * the all-reduces run over an RCCL communicator made from `id` (ncclCommInitRank);
  * asw_comm_unique_id makes the id on one rank (ncclGetUniqueId) and the caller
  * shares it with the others (MPI, torch.distributed, a file).  Every rank returns
- * the whole frame's outputs. */
+ * the whole frame's maps and images; the one exception is asw_outputs.cost, which
+ * a rank fills only at its own planes [d_begin, d_end) (asw_ctx_shard) and leaves
+ * untouched elsewhere (the volume is never gathered).
+ * The cross-device RCCL path (distinct GPUs, nranks > 1, or asw_create_multi with
+ * distinct ids) runs the same protocol as the tested one-rank and same-device
+ * paths; it has not been executed on a multi-GPU box by this project's tests. */
 #define ASW_COMM_ID_BYTES 128
 int asw_comm_unique_id(uint8_t id[ASW_COMM_ID_BYTES]);
 int asw_create_rank(const asw_params *p, int hip_device, int rank, int nranks, const uint8_t id[ASW_COMM_ID_BYTES],

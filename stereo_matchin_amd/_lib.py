@@ -157,6 +157,7 @@ SIGNATURES = {
     "asw_set_refine": (I, [P, RP]),
     "asw_set_graph": (I, [P, I]),
     "asw_tune_set": (I, [I, I]),
+    "asw_pass_kernel": (I, [I, I, ctypes.c_char_p, I]),
     "asw_device_name": (I, [I, ctypes.c_char_p, I]),
     "asw_create": (I, [PP, I, ctypes.POINTER(P)]),
     "asw_destroy": (I, [P]),

@@ -4,6 +4,10 @@
 // by the Makefile) so they compile in parallel.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
 #include "asw_common.h"
 
 namespace asw {
@@ -31,14 +35,29 @@ int set_pass_variant(int v) {
     return old;
 }
 
-int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                float *den, int dm, hipStream_t st, const RawSrc *raw) {
-    if (dm != 0 && !den) return ASW_E_INVALID;
-    // the pass kernels address the cost volume with 32-bit buffer offsets of up to
-    // ~2T+16 rows from a per-chunk base, and a support array from its base
+namespace {
+std::mutex g_note_mu;
+char g_note[2][3][96];  // [dir][den mode]
+}  // namespace
+
+void note_pass_kernel(int dir, int dm, const char *kernel, int T, const char *shape, bool nt) {
+    if (dir < 0 || dir > 1 || dm < 0 || dm > 2) return;
+    std::lock_guard<std::mutex> lk(g_note_mu);
+    std::snprintf(g_note[dir][dm], sizeof g_note[dir][dm], "%s<T=%d,%s,DM=%d%s>", kernel, T, shape, dm,
+                  nt ? ",nt" : "");
+}
+
+int pass_shape_check(const asw_params *p) {
     const long long rowbytes = (long long)p->width * asw_disp_pitch(p) * 4;
     if (rowbytes * (2LL * p->taps + 16) >= (1LL << 31)) return ASW_E_UNSUPPORTED;
     if ((long long)asw_support_bytes(p) >= (1LL << 31)) return ASW_E_UNSUPPORTED;
+    return ASW_OK;
+}
+
+int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                float *den, int dm, hipStream_t st, const RawSrc *raw) {
+    if (dm != 0 && !den) return ASW_E_INVALID;
+    if (const int s = pass_shape_check(p)) return s;
 #ifdef ASW_DEV_TAPS  // development build (make DEV=1): one ring-kernel tap count only
     if (p->taps == ASW_DEV_TAPS) return agg::launch_pass_t<ASW_DEV_TAPS>(p, dir, wl, wr, cin, cout, den, dm, st, raw);
     if (raw) return ASW_E_UNSUPPORTED;
@@ -64,3 +83,12 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
 }
 
 }  // namespace asw
+
+extern "C" int asw_pass_kernel(int dir, int den_mode, char *buf, int len) {
+    if (dir < 0 || dir > 1 || den_mode < 0 || den_mode > 2 || !buf || len < 1) return ASW_E_INVALID;
+    std::lock_guard<std::mutex> lk(asw::g_note_mu);
+    const char *n = asw::g_note[dir][den_mode];
+    if (!n[0]) return ASW_E_INVALID;
+    std::snprintf(buf, (size_t)len, "%s", n);
+    return ASW_OK;
+}

@@ -55,6 +55,7 @@ int launch_pass_any(const asw_params *p, int dir, const float *wl, const float *
     const unsigned nb = (unsigned)((S + 3) / 4);
     hipLaunchKernelGGL(k_pass_any, dim3(nb), dim3(256), 0, st, wl, wr, cin, cout, den, p->width, p->height,
                        asw_disp_pitch(p), p->d_begin, p->taps, asw_tap_pitch(p), dir, dm == ASW_DEN_WRITE ? 1 : 0);
+    note_pass_kernel(dir, dm, "k_pass_any", p->taps, "wave/pixel", false);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_hip_error(e);

@@ -44,6 +44,13 @@ struct RawSrc {
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                 float *den, int dm, hipStream_t st, const RawSrc *raw = nullptr);
 int set_pass_variant(int v);
+// records the instantiation a pass launch of (dir, dm) runs (asw_pass_kernel)
+void note_pass_kernel(int dir, int dm, const char *kernel, int T, const char *shape, bool nt);
+// ASW_OK when the pass kernels can address a (shard) context of this shape: they use
+// 32-bit buffer offsets of up to ~2T+16 cost rows from a per-chunk base and a support
+// array from its base; ASW_E_UNSUPPORTED otherwise (checked at asw_create, before
+// any allocation, and by every pass launch)
+int pass_shape_check(const asw_params *p);
 
 // lane-per-pixel WTA scan (asw_refine.hip): mode 0 = asw_WTA, 1 = asw_WTA_REF
 // lane-per-pixel d-sharded WTA halves (ref = NULL: asw_WTA; else asw_WTA_REF's penalty)

@@ -338,7 +338,10 @@ int create_ctx(const asw_params *p, const int *devs, int n, int shard0, int tota
         sh.device = devs[i];
         sh.p = c->p;
         shard_range(p->ndisp, shard0 + i, total, &sh.p.d_begin, &sh.p.d_end);
-        chain(alloc_shard(sh, comm != COMM_NONE));
+        // a shape the pass kernels cannot address fails here, before tens of GB are
+        // allocated, not at the first pass
+        chain(asw::pass_shape_check(&sh.p));
+        if (s == ASW_OK) chain(alloc_shard(sh, comm != COMM_NONE));
     }
     if (s == ASW_OK && comm == COMM_LOCAL) {
         chain(hipSetDevice(devs[0]) == hipSuccess ? ASW_OK : ASW_E_HIP);
@@ -351,8 +354,9 @@ int create_ctx(const asw_params *p, const int *devs, int n, int shard0, int tota
         ncclComm_t comms[kMaxShards] = {};
         ncclResult_t r;
         if (id) {  // one process per GPU
-            HIPCHK(hipSetDevice(devs[0]));
-            r = ncclCommInitRank(&comms[0], total, *id, shard0);
+            const hipError_t e = hipSetDevice(devs[0]);
+            r = e == hipSuccess ? ncclCommInitRank(&comms[0], total, *id, shard0) : ncclInvalidUsage;
+            if (e != hipSuccess) asw::set_hip_error(e);
         } else {
             r = ncclCommInitAll(comms, n, devs);
         }
@@ -571,8 +575,13 @@ int graph_run(hipStream_t st, hipGraph_t *g, hipGraphExec_t *gx, F &&fn) {
             if (cap) (void)hipGraphDestroy(cap);
             return s != ASW_OK ? s : hip_fail(e);
         }
+        const hipError_t ei = hipGraphInstantiate(gx, cap, nullptr, nullptr, 0);
+        if (ei != hipSuccess) {  // nothing kept: the next call captures afresh
+            (void)hipGraphDestroy(cap);
+            *gx = nullptr;
+            return hip_fail(ei);
+        }
         *g = cap;
-        HIPCHK(hipGraphInstantiate(gx, cap, nullptr, nullptr, 0));
     }
     HIPCHK(hipGraphLaunch(*gx, st));
     return ASW_OK;

@@ -145,6 +145,9 @@ template <int Q>
 __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *__restrict__ lut, int W, int H,
                                                  int T) {
     using f4 = float __attribute__((ext_vector_type(4)));
+    // 4 waves x 64 pixels x Q float4 = 4 KiB per Q: Q = 17 (T 65-68) takes 68 KiB,
+    // which only the 160 KiB LDS of gfx950 holds (the build targets gfx950 only)
+    static_assert(4 * 64 * Q * 16 <= 160 * 1024, "k_support staging tile exceeds the gfx950 LDS");
     __shared__ f4 stg[4][64 * Q];  // per wave: its 64 pixels' Q float4, in output order
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x0 = blockIdx.x * 64;
@@ -575,7 +578,9 @@ using namespace asw;
 // ===========================================================================
 extern "C" {
 
-int asw_abi_version(void) { return 1; }
+// 2: asw_outputs gained disp16 / lr16 and asw_timings gained exchange (round 2);
+// asw_create rejects shapes the pass kernels cannot address (ASW_E_UNSUPPORTED)
+int asw_abi_version(void) { return ASW_ABI_VERSION; }
 
 static int g_wta_variant = 0;
 

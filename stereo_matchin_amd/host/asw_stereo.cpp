@@ -186,7 +186,12 @@ int main(int argc, char **argv) {
             ++failures;
             continue;
         }
-        const bool refine = o.refine > 0 && p.lr_check && o.devices.size() == 1 && !wide;
+        // the loop runs on d-sharded contexts too (asw_set_refine: its asw_WTA_REF scan is
+        // exchanged like the WTA); it feeds back 8-bit codes, so D > 256 has none
+        const bool refine = o.refine > 0 && p.lr_check && !wide;
+        if (o.refine > 0 && !refine)
+            std::fprintf(stderr, "%s: refinement skipped (%s)\n", folder.c_str(),
+                         !p.lr_check ? "it needs the LR check" : "D > 256: the loop re-reads 8-bit codes");
         if (refine) {
             asw_refine_params rp;
             asw_refine_params_default(&rp);

@@ -165,6 +165,16 @@ def _pass(p: AswParams, direction: int, supp_left, supp_right, cost_in, out, den
     return out
 
 
+def pass_kernel(direction: int, den_mode: int) -> str | None:
+    """Name of the kernel instantiation the latest aggregation-pass launch of
+    (direction, den_mode) in this process ran (asw_pass_kernel), or None."""
+    import ctypes
+    buf = ctypes.create_string_buffer(128)
+    if _lib.lib().asw_pass_kernel(direction, den_mode, buf, len(buf)) != 0:
+        return None
+    return buf.value.decode()
+
+
 def asw_vCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None, den=None, den_mode: int = 0):
     """One vertical weighted-aggregation pass (K/asw_vcost_aggregation.cl:11-44).
 

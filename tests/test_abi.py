@@ -26,7 +26,7 @@ def test_every_header_symbol_is_exported(L):
 
 
 def test_abi_version(L):
-    assert L.lib().asw_abi_version() == 1
+    assert L.lib().asw_abi_version() == 2
 
 
 def test_default_params_are_the_reference_values(L):

@@ -207,6 +207,27 @@ def test_cli_tsukuba_reproduces_reference_png(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_devices_refine_matches_reference(tmp_path):
+    """--devices 0,0 with the default --refine 6: the d-sharded refinement writes the
+    reference's asw_disparity.png and asw_consistency_post-reff.png (main.cpp:617-631),
+    byte-exact against the committed tsukuba files (--devices used to drop
+    refinement silently)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "tsukuba.npz"))
+    d = tmp_path / "tsukuba"
+    d.mkdir()
+    PIL.fromarray(z["left"]).save(d / "im1.png")
+    PIL.fromarray(z["right"]).save(d / "im5.png")
+    (tmp_path / "pics.txt").write_text("tsukuba/im1.png\ntsukuba/im5.png\n")
+    r = subprocess.run([CLI, "--pics", str(tmp_path / "pics.txt"), "--runs", "1", "--devices", "0,0"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "skipped" not in r.stderr
+    for name, key in (("asw_disparity.png", "disp_final"), ("asw_consistency_post-reff.png", "lr_post_red"),
+                      ("asw_consistency_pre-reff.png", "lr_red")):
+        np.testing.assert_array_equal(np.asarray(PIL.open(d / name).convert("RGB")), z[key], err_msg=name)
+
+
+@pytest.mark.gpu
 def test_cli_devices_and_png16(tmp_path):
     """--devices 0,0 (two d-shards on one GPU, asw_create_multi) reproduces the one-GPU
     images; --png16 writes the 16-bit disparity maps (d_ref; 65535 = LR-inconsistent)."""
