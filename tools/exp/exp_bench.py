@@ -1,0 +1,129 @@
+"""Drives tools/exp/libexp.so (experimental pass kernels) on the real C4 inputs and
+checks every experiment bit-exact against the production pass.  Not part of the product.
+
+    python tools/exp/exp_bench.py [--reps 8]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from stereo_matchin_amd import StereoMatcher, make_params  # noqa: E402
+from stereo_matchin_amd import kernels as K  # noqa: E402
+from stereo_matchin_amd.synthetic import make_pair  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--v", action="store_true", help="V-pass experiments")
+    ap.add_argument("--h", action="store_true", help="H-pass experiments")
+    args = ap.parse_args()
+    W, H, D, T = 1920, 1080, 256, 35
+    dev = torch.device("cuda:0")
+    Lh, Rh, _ = make_pair(W, H, D, 0)
+    p = make_params(W, H, ndisp=D, taps=T, iters=7)
+    m = StereoMatcher(p, dev)
+    m.raw_and_support(torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev))
+    # a realistic H input: one V pass of the raw cost
+    cin = torch.empty_like(m.c0)
+    K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=cin)
+    den = torch.empty_like(cin)
+    ref = torch.empty_like(cin)
+    K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=ref, den=den, den_mode=1)
+    torch.cuda.synchronize()
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp.so"))
+    pp = ctypes.byref(p)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    out = torch.empty_like(cin)
+
+    def h(nkw, dm, kbg0, nkbg, st):
+        rc = lib.exp_h11(nkw, dm, pp, P(m.whl), P(m.whr), P(cin), P(out), P(den), kbg0, nkbg,
+                         ctypes.c_void_p(st.cuda_stream))
+        assert rc == 0, rc
+
+    # V pass experiments: the production den-write pass gives den_v, the production
+    # den-read pass the reference output
+    if args.v:
+        denv = torch.empty_like(cin)
+        refv = torch.empty_like(cin)
+        K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=refv, den=denv, den_mode=1)
+        torch.cuda.synchronize()
+        vres = {}
+        vexps = [("prod_read", None, 2, 0), ("v11_read", 2, 2, 0), ("v11_read_s1", 2, 2, 1), ("v11_read_s3", 2, 2, 3),
+                 ("prod_none", None, 0, 0), ("v11_none", 2, 0, 0)]
+        for rep in range(args.reps + 1):
+            for name, kind, dm, ns in vexps:
+                out.zero_()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                if kind is None:
+                    K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=denv if dm else None, den_mode=dm)
+                else:
+                    rc = lib.exp_v11(dm, ns, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                    assert rc == 0, rc
+                e1.record()
+                torch.cuda.synchronize()
+                if rep == 0:
+                    if not torch.equal(out, refv):
+                        bad = (out != refv).nonzero()
+                        print(json.dumps({"exp": name, "error": "differs", "n": int(bad.shape[0]),
+                                          "first": bad[:4].tolist()}), flush=True)
+                else:
+                    vres.setdefault(name, []).append(e0.elapsed_time(e1))
+        for name, ts in vres.items():
+            print(json.dumps({"exp": name, "ms_median": round(float(np.median(ts)), 4), "ms_min": round(min(ts), 4)}),
+                  flush=True)
+        if not args.h:
+            return
+    nkb = 4
+    exps = {
+        "read_nkw4": [(4, 2, 0, 1, 0)],
+        "none_nkw4": [(4, 0, 0, 1, 0)],
+        "read_nkw1": [(1, 2, 0, 4, 0)],
+        "none_nkw1": [(1, 0, 0, 4, 0)],
+        "mix2_nkw2_2streams": [(2, 2, 0, 1, 0), (2, 0, 1, 1, 1)],
+        "mix2_nkw2_serial": [(2, 2, 0, 1, 0), (2, 0, 1, 1, 0)],
+        "mix3r1n_nkw1_2streams": [(1, 2, 0, 3, 0), (1, 0, 3, 1, 1)],
+        "mix1r3n_nkw1_2streams": [(1, 2, 0, 1, 0), (1, 0, 1, 3, 1)],
+        "mix2_nkw1_2streams": [(1, 2, 0, 2, 0), (1, 0, 2, 2, 1)],
+    }
+    del nkb
+    res = {k: [] for k in exps}
+    cur = torch.cuda.current_stream()
+    for rep in range(args.reps + 1):
+        for name, launches in exps.items():
+            out.zero_()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cur)
+            for st in (s1, s2):
+                st.wait_event(e0)
+            for nkw, dm, kbg0, nkbg, si in launches:
+                h(nkw, dm, kbg0, nkbg, (s1, s2)[si])
+            for st in (s1, s2):
+                cur.wait_stream(st)
+            e1.record(cur)
+            torch.cuda.synchronize()
+            if rep == 0:
+                ok = torch.equal(out, ref)
+                if not ok:
+                    print(json.dumps({"exp": name, "error": "differs from the production pass"}), flush=True)
+            else:
+                res[name].append(e0.elapsed_time(e1))
+    for name, ts in res.items():
+        print(json.dumps({"exp": name, "ms_median": round(float(np.median(ts)), 4), "ms_min": round(min(ts), 4)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
