@@ -137,16 +137,18 @@ def cpu_baseline(Lh, Rh, D, T, iters, rows, lr_mode):
     }
 
 
-def h_kernel_name(W, H, nloc, T):
+def h_kernel_name(W, H, nloc, T, otf=False):
     """The H pass kernel launch_dm (asw_aggregate_impl.h) selects for this shape: k_hpass11
-    when its row-segment grid has >= 8192 waves, else k_hpass9."""
+    when its row-segment grid has >= 8192 waves, else k_hpass9 (_otf: right weights
+    computed on the fly)."""
     U = T + 3
     while U % 4:
         U += 1
     seg = (240 + U // 2) // U * U
     nkb = (nloc + 63) // 64
     waves = H * ((W + seg - 1) // seg) * nkb
-    return "k_hpass11<DM_READ>" if waves >= 8192 else "k_hpass9<DM_READ>"
+    sfx = "_otf" if otf else ""
+    return f"k_hpass11{sfx}<DM_READ>" if waves >= 8192 else f"k_hpass9{sfx}<DM_READ>"
 
 
 def load_traffic(path, workload, n_gpus, kernel):
@@ -312,6 +314,25 @@ def main():
                     it[name] += 1
                     prev = e
             frame_ms.append(ev[0][1].elapsed_time(ev[-1][1]))
+    # den-none passes beside the shipped den-read ones (report both and ship
+    # the faster): one V and one H pass without the cached denominators, on the
+    # matcher's own buffers, after the timed region (not part of `value`)
+    v_none, h_none = [], []
+    if not frame and world == 1 and iters >= 2:
+        from stereo_matchin_amd import kernels as K
+        for _ in range(3):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+            K.asw_vCostAggregation(m.p, m.wvl, m.wvr, m.c0, out=m.c1)
+            e[1].record()
+            if m.otf:
+                K.asw_hCostAggregation_otf(m.p, m.whl, m.right, m.lut, m.c1, out=m.c0)
+            else:
+                K.asw_hCostAggregation(m.p, m.whl, m.whr, m.c1, out=m.c0)
+            e[2].record()
+            torch.cuda.synchronize()
+            v_none.append(e[0].elapsed_time(e[1]))
+            h_none.append(e[1].elapsed_time(e[2]))
     mean = lambda xs: float(np.mean(xs)) if xs else float("nan")  # noqa: E731
     all_pass = v_rd + h_rd + v_wr + h_wr
     stats = torch.tensor([elapsed, mean(v_rd), mean(h_rd), mean(v_wr), mean(h_wr), mean(all_pass),
@@ -328,7 +349,7 @@ def main():
         maps_per_s = n_maps / (span_sum / 1e3) if frame else n_maps / elapsed
         dom = "v" if (v_avg >= h_avg or h_avg != h_avg) else "h"
         dom_ms = v_avg if dom == "v" else h_avg
-        kname = "k_vpass10<DM_READ>" if dom == "v" else h_kernel_name(W, H, nloc, T)
+        kname = "k_vpass10<DM_READ>" if dom == "v" else h_kernel_name(W, H, nloc, T, getattr(getattr(m, "matcher", m), "otf", False))
         out = {
             "metric": METRIC,
             "value": round(maps_per_s, 4),
@@ -359,6 +380,13 @@ def main():
                          "v_read_ms": round(v_avg, 4), "v_read_frac": round(gbs(v_avg) / HBM_PEAK_GBS, 4),
                          "h_read_ms": round(h_avg, 4), "h_read_frac": round(gbs(h_avg) / HBM_PEAK_GBS, 4),
                          "v_write_ms": round(vw_avg, 4), "h_write_ms": round(hw_avg, 4),
+                         "v_none_ms": round(float(np.median(v_none)), 4) if v_none else None,
+                         "v_none_frac": round(gbs(float(np.median(v_none))) / HBM_PEAK_GBS, 4) if v_none else None,
+                         "h_none_ms": round(float(np.median(h_none)), 4) if h_none else None,
+                         "h_none_frac": round(gbs(float(np.median(h_none))) / HBM_PEAK_GBS, 4) if h_none else None,
+                         "den_modes": "the frame ships cached denominators (den-read) for r >= 2: den-none "
+                                      "(v/h_none, 3 VALU per voxel-tap instead of 2, 2.1 GB less traffic) is "
+                                      "timed beside it outside the timed region",
                          "all_pass_mean_ms": round(pass_avg, 4),
                          "all_pass_frac": round(gbs(pass_avg) / HBM_PEAK_GBS, 4),
                          "timing": "frame API: asw_timings per-direction means over all r passes" if frame else

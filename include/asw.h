@@ -105,7 +105,9 @@ int asw_support(const asw_params *p, int dir, const uint8_t *img_rgba, const flo
                 void *stream);
 
 /* the four support arrays of a frame in one launch (asw_vSupport and asw_hSupport of
- * both images, main.cpp:469-484): bit-identical to four asw_support calls. */
+ * both images, main.cpp:469-484): bit-identical to four asw_support calls.  Any of
+ * the four outputs may be NULL (not computed; e.g. whr when the H passes compute it
+ * on the fly, asw_aggregate_pass_otf), at least one must be given. */
 int asw_support_all(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba, const float *lut,
                     float *wvl, float *whl, float *wvr, float *whr, void *stream);
 
@@ -137,6 +139,19 @@ int asw_aggregate_pass(const asw_params *p, int dir, const float *wl, const floa
 #define ASW_DEN_READ 2  /* take den from `den` (written by a DEN_WRITE pass of this direction) */
 int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin,
                            float *cout, float *den, int den_mode, void *stream);
+
+/* The H pass (asw_hCostAggregation, K/asw_hcost_aggregation.cl:12-44) with the RIGHT
+ * support weights computed on the fly: instead of reading the
+ * asw_hSupport array of the right image (K/asw_hsupport.cl:19-27, main.cpp:482-484),
+ * the pass computes each weight from `right_rgba` (device RGBA8) and the support LUT
+ * (asw_support_lut) as asw_support does, so that array is never written nor read.
+ * Bit-identical to asw_aggregate_pass_den with wr = asw_support(H, right).  H only,
+ * RGB contexts, tap counts with ring kernels (3, 5, 7, 9, 15, 33, 35, 51; see
+ * asw_pass_otf_supported): ASW_E_UNSUPPORTED otherwise. */
+int asw_aggregate_pass_otf(const asw_params *p, int dir, const float *wl, const uint8_t *right_rgba,
+                           const float *lut, const float *cin, float *cout, float *den, int den_mode, void *stream);
+/* 1 when asw_aggregate_pass_otf supports (p, dir), else 0 */
+int asw_pass_otf_supported(const asw_params *p, int dir);
 
 /* The first V pass of main.cpp:494-500 with asw_Aggr (main.cpp:463-466,
  * K/asw_aggr.cl:3-23) fused: each window element's raw AD/TAD cost is computed

@@ -133,6 +133,8 @@ SIGNATURES = {
     "asw_aggregate_pass": (I, [PP, I, P, P, P, P, P]),
     "asw_aggregate_pass_den": (I, [PP, I, P, P, P, P, P, I, P]),
     "asw_aggregate_pass_raw": (I, [PP, P, P, P, P, P, P, I, P]),
+    "asw_aggregate_pass_otf": (I, [PP, I, P, P, P, P, P, P, I, P]),
+    "asw_pass_otf_supported": (I, [PP, I]),
     "asw_aggregate": (I, [PP, P, P, P, P, P, P, P]),
     "asw_aggregate_den": (I, [PP, P, P, P, P, P, P, P, P, P]),
     "asw_wta": (I, [PP, P, P, P, P, P, P, P, P]),

@@ -15,13 +15,13 @@ namespace agg {
 int g_pass_variant = 0;
 template <int T, int DM>
 int launch_pass_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                   float *den, hipStream_t st, const RawSrc *raw);
+                   float *den, hipStream_t st, const RawSrc *raw, const OtfSrc *otf);
 template <int T>
 int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                  float *den, int dm, hipStream_t st, const RawSrc *raw) {
-    if (dm == 1) return launch_pass_tm<T, 1>(p, dir, wl, wr, cin, cout, den, st, raw);
-    if (dm == 2) return launch_pass_tm<T, 2>(p, dir, wl, wr, cin, cout, den, st, raw);
-    return launch_pass_tm<T, 0>(p, dir, wl, wr, cin, cout, den, st, raw);
+                  float *den, int dm, hipStream_t st, const RawSrc *raw, const OtfSrc *otf) {
+    if (dm == 1) return launch_pass_tm<T, 1>(p, dir, wl, wr, cin, cout, den, st, raw, otf);
+    if (dm == 2) return launch_pass_tm<T, 2>(p, dir, wl, wr, cin, cout, den, st, raw, otf);
+    return launch_pass_tm<T, 0>(p, dir, wl, wr, cin, cout, den, st, raw, otf);
 }
 }  // namespace agg
 
@@ -54,19 +54,28 @@ int pass_shape_check(const asw_params *p) {
     return ASW_OK;
 }
 
+bool ring_taps(int T) {
+#ifdef ASW_DEV_TAPS
+    return T == ASW_DEV_TAPS;
+#else
+    return T == 3 || T == 5 || T == 7 || T == 9 || T == 15 || T == 33 || T == 35 || T == 51;
+#endif
+}
+
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                float *den, int dm, hipStream_t st, const RawSrc *raw) {
+                float *den, int dm, hipStream_t st, const RawSrc *raw, const OtfSrc *otf) {
     if (dm != 0 && !den) return ASW_E_INVALID;
     if (const int s = pass_shape_check(p)) return s;
+    if (otf && (dir != ASW_DIR_H || raw || !ring_taps(p->taps))) return ASW_E_UNSUPPORTED;
 #ifdef ASW_DEV_TAPS  // development build (make DEV=1): one ring-kernel tap count only
-    if (p->taps == ASW_DEV_TAPS) return agg::launch_pass_t<ASW_DEV_TAPS>(p, dir, wl, wr, cin, cout, den, dm, st, raw);
+    if (p->taps == ASW_DEV_TAPS) return agg::launch_pass_t<ASW_DEV_TAPS>(p, dir, wl, wr, cin, cout, den, dm, st, raw, otf);
     if (raw) return ASW_E_UNSUPPORTED;
     return launch_pass_any(p, dir, wl, wr, cin, cout, den, dm, st);
 #endif
     switch (p->taps) {
 #define ASW_CASE(TT) \
     case TT:         \
-        return agg::launch_pass_t<TT>(p, dir, wl, wr, cin, cout, den, dm, st, raw);
+        return agg::launch_pass_t<TT>(p, dir, wl, wr, cin, cout, den, dm, st, raw, otf);
         ASW_CASE(3)
         ASW_CASE(5)
         ASW_CASE(7)

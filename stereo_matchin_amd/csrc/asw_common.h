@@ -39,10 +39,20 @@ struct RawSrc {
     const uint8_t *left, *right;
 };
 
+// right support weights of an H pass computed on the fly (asw_aggregate_pass_otf):
+// the right RGBA8 image and the support LUT (asw_support_lut)
+struct OtfSrc {
+    const uint8_t *right;
+    const float *lut;
+};
+
 // one aggregation pass over every local plane (asw_aggregate.hip)
 // den/dm: cached-denominator mode (ASW_DEN_*; den = NULL with ASW_DEN_NONE)
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                float *den, int dm, hipStream_t st, const RawSrc *raw = nullptr);
+                float *den, int dm, hipStream_t st, const RawSrc *raw = nullptr, const OtfSrc *otf = nullptr);
+// the tap counts with ring kernels (the ones asw_aggregate_pass_otf and the fused
+// raw-cost pass support)
+bool ring_taps(int T);
 int set_pass_variant(int v);
 // records the instantiation a pass launch of (dir, dm) runs (asw_pass_kernel)
 void note_pass_kernel(int dir, int dm, const char *kernel, int T, const char *shape, bool nt);

@@ -39,6 +39,7 @@ struct Shard {
     float *wvl = nullptr, *wvr = nullptr, *whl = nullptr, *whr = nullptr;  // [H][W][Tp]
     float *c0 = nullptr, *c1 = nullptr;                                    // [H][W][Dp]
     float *den_v = nullptr, *den_h = nullptr;  // cached denominators (iters >= 2)
+    bool otf = false;  // the H passes compute the right weights on the fly (whr not allocated)
     // d-sharded WTA (more than one shard in the frame)
     int64_t *key = nullptr, *key_g = nullptr, *tkey = nullptr, *tkey_g = nullptr;
     float *m1 = nullptr, *m2 = nullptr, *t1 = nullptr, *t2 = nullptr, *m2_g = nullptr, *t2_g = nullptr;
@@ -259,7 +260,12 @@ int alloc_shard(Shard &s, bool sharded) {
     ASWCHK(dev_alloc(&s.wvl, asw_support_bytes(p)));
     ASWCHK(dev_alloc(&s.wvr, asw_support_bytes(p)));
     ASWCHK(dev_alloc(&s.whl, asw_support_bytes(p)));
-    ASWCHK(dev_alloc(&s.whr, asw_support_bytes(p)));
+    // the right H weights can be computed inside the H passes
+    // (asw_aggregate_pass_otf, the array then never built): bit-identical but measured
+    // slower at C4 (H den-read 2.30 against 1.42 ms), so only on request (ASW_OTF=1)
+    const char *otf_env = std::getenv("ASW_OTF");
+    s.otf = otf_env && otf_env[0] == '1' && asw_pass_otf_supported(p, ASW_DIR_H) != 0;
+    if (!s.otf) ASWCHK(dev_alloc(&s.whr, asw_support_bytes(p)));
     ASWCHK(dev_alloc(&s.c0, asw_cost_bytes(p)));
     ASWCHK(dev_alloc(&s.c1, asw_cost_bytes(p)));
     if (p->iters >= 2) {  // the den of a direction is written by its first pass and read by the r-1 others
@@ -316,6 +322,14 @@ int create_ctx(const asw_params *p, const int *devs, int n, int shard0, int tota
     ASWCHK(asw_params_check(p));
     if (p->d_begin != 0 || (p->d_end >= 0 && p->d_end != p->ndisp)) return ASW_E_INVALID;  // contexts shard themselves
     if (n < 1 || n > kMaxShards || total < n || total > p->ndisp) return ASW_E_INVALID;
+    // a shape the pass kernels cannot address fails here, before any device call or
+    // allocation (tens of GB for an 8K frame), not at the first pass
+    for (int i = 0; i < n; ++i) {
+        asw_params sp = *p;
+        sp.d_end = p->ndisp;
+        shard_range(p->ndisp, shard0 + i, total, &sp.d_begin, &sp.d_end);
+        ASWCHK(asw::pass_shape_check(&sp));
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
     for (int i = 0; i < n; ++i)
@@ -338,10 +352,7 @@ int create_ctx(const asw_params *p, const int *devs, int n, int shard0, int tota
         sh.device = devs[i];
         sh.p = c->p;
         shard_range(p->ndisp, shard0 + i, total, &sh.p.d_begin, &sh.p.d_end);
-        // a shape the pass kernels cannot address fails here, before tens of GB are
-        // allocated, not at the first pass
-        chain(asw::pass_shape_check(&sh.p));
-        if (s == ASW_OK) chain(alloc_shard(sh, comm != COMM_NONE));
+        chain(alloc_shard(sh, comm != COMM_NONE));
     }
     if (s == ASW_OK && comm == COMM_LOCAL) {
         chain(hipSetDevice(devs[0]) == hipSuccess ? ASW_OK : ASW_E_HIP);
@@ -418,14 +429,15 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         ASWCHK(asw_support_lab(p, ASW_DIR_H, s.lab_r, s.whr, st));
     } else {
         ASWCHK(asw_support_lut(p, s.lut, st));
-        ASWCHK(asw_support_all(p, s.left, s.right, s.lut, s.wvl, s.whl, s.wvr, s.whr, st));
+        ASWCHK(asw_support_all(p, s.left, s.right, s.lut, s.wvl, s.whl, s.wvr, s.otf ? nullptr : s.whr, st));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0], st));
     for (int it = 0; it < p->iters; ++it) {
         const int dm = !s.den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
         ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, s.wvl, s.wvr, s.c0, s.c1, s.den_v, dm, st));
         if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0 + 2 * it + 1], st));
-        ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, s.whl, s.whr, s.c1, s.c0, s.den_h, dm, st));
+        if (s.otf) ASWCHK(asw_aggregate_pass_otf(p, ASW_DIR_H, s.whl, s.right, s.lut, s.c1, s.c0, s.den_h, dm, st));
+        else ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, s.whl, s.whr, s.c1, s.c0, s.den_h, dm, st));
         if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0 + 2 * it + 2], st));
     }
     return ASW_OK;

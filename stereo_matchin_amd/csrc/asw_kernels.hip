@@ -717,18 +717,21 @@ int asw_support(const asw_params *p, int dir, const uint8_t *img, const float *l
 int asw_support_all(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut, float *wvl,
                     float *whl, float *wvr, float *whr, void *stream) {
     ASW_CHECK_PARAMS(p);
-    if (!left || !right || !lut || !wvl || !whl || !wvr || !whr) return ASW_E_INVALID;
+    if (!left || !right || !lut || !(wvl || whl || wvr || whr)) return ASW_E_INVALID;
     if (p->color_space != ASW_COLOR_RGB) return ASW_E_INVALID;
     SupportJobs jobs{};
     const uchar4 *img[4] = {reinterpret_cast<const uchar4 *>(left), reinterpret_cast<const uchar4 *>(left),
                             reinterpret_cast<const uchar4 *>(right), reinterpret_cast<const uchar4 *>(right)};
     float *w[4] = {wvl, whl, wvr, whr};
+    int n = 0;
     for (int j = 0; j < 4; ++j) {
-        jobs.img[j] = img[j];
-        jobs.w[j] = w[j];
-        jobs.dir[j] = (j & 1) ? ASW_DIR_H : ASW_DIR_V;
+        if (!w[j]) continue;  // an array the caller computes on the fly (asw_aggregate_pass_otf)
+        jobs.img[n] = img[j];
+        jobs.w[n] = w[j];
+        jobs.dir[n] = (j & 1) ? ASW_DIR_H : ASW_DIR_V;
+        ++n;
     }
-    return launch_support(p, jobs, 4, lut, stream);
+    return launch_support(p, jobs, n, lut, stream);
 }
 
 int asw_lab(const asw_params *p, const uint8_t *img, float *lab, void *stream) {
@@ -767,6 +770,22 @@ int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const 
     if (den_mode < ASW_DEN_NONE || den_mode > ASW_DEN_READ) return ASW_E_INVALID;
     if (den_mode != ASW_DEN_NONE && (!den || den == cin || den == cout)) return ASW_E_INVALID;
     return asw::launch_pass(p, dir, wl, wr, cin, cout, den, den_mode, (hipStream_t)stream);
+}
+
+int asw_aggregate_pass_otf(const asw_params *p, int dir, const float *wl, const uint8_t *right_rgba, const float *lut,
+                           const float *cin, float *cout, float *den, int den_mode, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!wl || !right_rgba || !lut || !cin || !cout || cin == cout) return ASW_E_INVALID;
+    if (den_mode < ASW_DEN_NONE || den_mode > ASW_DEN_READ) return ASW_E_INVALID;
+    if (den_mode != ASW_DEN_NONE && (!den || den == cin || den == cout)) return ASW_E_INVALID;
+    if (dir != ASW_DIR_H || p->color_space != ASW_COLOR_RGB || !asw::ring_taps(p->taps)) return ASW_E_UNSUPPORTED;
+    const asw::OtfSrc otf{right_rgba, lut};
+    return asw::launch_pass(p, dir, wl, nullptr, cin, cout, den, den_mode, (hipStream_t)stream, nullptr, &otf);
+}
+
+int asw_pass_otf_supported(const asw_params *p, int dir) {
+    if (!p || asw_params_check(p) != ASW_OK) return 0;
+    return dir == ASW_DIR_H && p->color_space == ASW_COLOR_RGB && asw::ring_taps(p->taps) ? 1 : 0;
 }
 
 int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,

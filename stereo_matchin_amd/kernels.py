@@ -111,7 +111,8 @@ def support_all(p: AswParams, left: torch.Tensor, right: torch.Tensor, lut: torc
     for img in (left, right):
         _expect(img, (p.height, p.width, 4), torch.uint8, "image")
     for w in (wvl, whl, wvr, whr):
-        _expect(w, support_shape(p), torch.float32, "out")
+        if w is not None:  # None: not computed (e.g. whr with the on-the-fly H pass)
+            _expect(w, support_shape(p), torch.float32, "out")
     _lib.check(_lib.lib().asw_support_all(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(lut), _ptr(wvl), _ptr(whl),
                                           _ptr(wvr), _ptr(whr), _stream(left.device)), "asw_support_all")
 
@@ -162,6 +163,34 @@ def _pass(p: AswParams, direction: int, supp_left, supp_right, cost_in, out, den
                                                  _ptr(cost_in), _ptr(out), _ptr(den), den_mode,
                                                  _stream(cost_in.device)),
                "asw_aggregate_pass_den")
+    return out
+
+
+def otf_supported(p: AswParams, direction: int = DIR_H) -> bool:
+    """asw_pass_otf_supported: the pass can compute its right weights on the fly."""
+    return bool(_lib.lib().asw_pass_otf_supported(ctypes.byref(p), direction))
+
+
+def asw_hCostAggregation_otf(p: AswParams, supp_left, right: torch.Tensor, lut: torch.Tensor, cost_in, out=None,
+                             den=None, den_mode: int = 0):
+    """The H pass with the right support weights computed on the fly from the right
+    image and the LUT (asw_aggregate_pass_otf): bit-identical to
+    asw_hCostAggregation(p, supp_left, asw_hSupport(p, right), ...)."""
+    _expect(supp_left, support_shape(p), torch.float32, "supp_left")
+    _expect(right, (p.height, p.width, 4), torch.uint8, "right")
+    _expect(lut, lut_shape(p), torch.float32, "lut")
+    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
+    if out is None:
+        out = torch.empty_like(cost_in)
+    _expect(out, cost_shape(p), torch.float32, "out")
+    if out.data_ptr() == cost_in.data_ptr():
+        raise ValueError("aggregation passes are out of place (cost_in != out)")
+    if den_mode:
+        _expect(den, cost_shape(p), torch.float32, "den")
+    _lib.check(_lib.lib().asw_aggregate_pass_otf(ctypes.byref(p), DIR_H, _ptr(supp_left), _ptr(right), _ptr(lut),
+                                                 _ptr(cost_in), _ptr(out), _ptr(den), den_mode,
+                                                 _stream(cost_in.device)),
+               "asw_aggregate_pass_otf")
     return out
 
 

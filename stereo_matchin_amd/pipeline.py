@@ -48,7 +48,8 @@ class StereoMatcher:
     (V, H) as volumes — written by the first pass of each direction, read by the
     other r-1 (ASW_DEN_*); bit-identical results, 2 more cost-sized buffers."""
 
-    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool = False):
+    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool = False,
+                 otf: bool | None = None):
         st = _lib.params_check(params)
         if st != _lib.ASW_OK:
             raise _lib.AswError(st, "asw_params_check")
@@ -59,10 +60,16 @@ class StereoMatcher:
         self.device = torch.device(device)
         dev = self.device
         self.lut = torch.empty(K.lut_shape(self.p), dtype=torch.float32, device=dev)
+        # otf: the H passes compute their right support weights from the right image
+        # (asw_aggregate_pass_otf), so whr is never built.  Off by default: bit-identical
+        # but measured slower (C4 H den-read 2.30 against 1.42 ms: the refill pipeline's
+        # registers cost the pass its latency cover; DESIGN.md §On-the-fly supports)
+        self.otf = False if otf is None else (otf and K.otf_supported(self.p))
+        self.right = None
         self.wvl = K.new_support(self.p, dev)
         self.wvr = K.new_support(self.p, dev)
         self.whl = K.new_support(self.p, dev)
-        self.whr = K.new_support(self.p, dev)
+        self.whr = None if self.otf else K.new_support(self.p, dev)
         self.c0 = K.new_cost(self.p, dev)
         self.c1 = K.new_cost(self.p, dev)
         self.den_v = self.den_h = None
@@ -86,7 +93,9 @@ class StereoMatcher:
             return
         K.support_lut(p, self.device, out=self.lut)
         # asw_vSupport / asw_hSupport of both images (main.cpp:469-484) in one launch
+        # (without asw_hSupport(right) when the H passes compute it on the fly)
         K.support_all(p, left, right, self.lut, self.wvl, self.whl, self.wvr, self.whr)
+        self.right = right
 
     def aggregate(self, events: list | None = None, images: tuple | None = None):
         """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515).
@@ -102,7 +111,11 @@ class StereoMatcher:
                 K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1, den=self.den_v, den_mode=dm)
             if events is not None:
                 events.append(("v", _record()))
-            K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0, den=self.den_h, den_mode=dm)
+            if self.otf:
+                K.asw_hCostAggregation_otf(p, self.whl, self.right, self.lut, self.c1, out=self.c0, den=self.den_h,
+                                           den_mode=dm)
+            else:
+                K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0, den=self.den_h, den_mode=dm)
             if events is not None:
                 events.append(("h", _record()))
         return self.c0

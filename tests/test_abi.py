@@ -107,6 +107,15 @@ def test_pass_rejects_volumes_past_32bit_offsets(L):
     q = L.default_params(3840, 2160, ndisp=512, taps=51)
     assert 3840 * 512 * 4 * (2 * 51 + 16) < 2 ** 31
     assert lib.asw_support_bytes(ctypes.byref(q)) < 2 ** 31
+    # the frame API rejects them at create, before any device call or allocation
+    # (an 8K D512 frame used to allocate tens of GB and fail at its
+    # first pass); a multi-shard context checks each shard's own pitch
+    ctx = ctypes.c_void_p()
+    big = L.default_params(7680, 4320, ndisp=512, taps=51)
+    assert lib.asw_create(ctypes.byref(big), 0, ctypes.byref(ctx)) == L.ASW_E_UNSUPPORTED and not ctx.value
+    ids = (ctypes.c_int * 2)(0, 0)
+    wide = L.default_params(7680, 64, ndisp=1280, taps=51)
+    assert lib.asw_create_multi(ctypes.byref(wide), ids, 2, ctypes.byref(ctx)) == L.ASW_E_UNSUPPORTED
 
 
 def test_frame_api_validates_before_allocating(L):
@@ -141,3 +150,22 @@ def test_missing_library_fails_loudly(tmp_path):
     env = dict(os.environ, ASW_LIB=str(tmp_path / "absent.so"))
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert "LOUD" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
+def test_pass_otf_support_and_errors(L):
+    """asw_aggregate_pass_otf (on-the-fly right H weights): H, RGB, ring tap counts only;
+    the unsupported combinations fail before any launch (no GPU needed)."""
+    lib = L.lib()
+    p = L.default_params(64, 32, ndisp=16, taps=35)
+    assert lib.asw_pass_otf_supported(ctypes.byref(p), 1) == 1
+    assert lib.asw_pass_otf_supported(ctypes.byref(p), 0) == 0  # V: not built
+    q = L.default_params(64, 32, ndisp=16, taps=11)  # no ring kernel for T = 11
+    assert lib.asw_pass_otf_supported(ctypes.byref(q), 1) == 0
+    r = L.default_params(64, 32, ndisp=16, taps=35, color_space=L.COLOR_LAB)
+    assert lib.asw_pass_otf_supported(ctypes.byref(r), 1) == 0
+    x = ctypes.c_void_p(1)
+    y = ctypes.c_void_p(2)
+    for pp, d in ((p, 0), (q, 1), (r, 1)):
+        assert lib.asw_aggregate_pass_otf(ctypes.byref(pp), d, x, x, x, x, y, None, L.DEN_NONE, None) == \
+            L.ASW_E_UNSUPPORTED
+    assert lib.asw_aggregate_pass_otf(ctypes.byref(p), 1, None, x, x, x, y, None, L.DEN_NONE, None) == L.ASW_E_INVALID

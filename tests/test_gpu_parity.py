@@ -248,6 +248,8 @@ def test_hpass_h11_bit_exact(gpu, oracle, T, H, W, D, d0, d1):
     sl, sr = oracle.support(Lh, T, 1), oracle.support(Rh, T, 1)
     wl, wr = K.asw_hSupport(p, _t(Lh, gpu)), K.asw_hSupport(p, _t(Rh, gpu))
     den = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+    den2 = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+    lut, R = K.support_lut(p, gpu), _t(Rh, gpu)
     old = _lib.lib().asw_tune_set(1, 4096)  # k_hpass11 below its frame-size threshold too
     try:
         for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
@@ -256,14 +258,59 @@ def test_hpass_h11_bit_exact(gpu, oracle, T, H, W, D, d0, d1):
             out = K.asw_hCostAggregation(p, wl, wr, _t(pixel_major(cin, Dp), gpu), den=den, den_mode=mode)
             got = plane_major(_np(out), d1 - d0)
             assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
+            # the same pass with the right weights computed on the fly
+            out = K.asw_hCostAggregation_otf(p, wl, R, lut, _t(pixel_major(cin, Dp), gpu), den=den2, den_mode=mode)
+            assert K.pass_kernel(1, mode).startswith(f"k_hpass11_otf<T={T}")
+            got = plane_major(_np(out), d1 - d0)
+            assert np.array_equal(got, want), ("otf", mode, np.argwhere(got != want)[:5])
     finally:
         _lib.lib().asw_tune_set(1, old)
 
 
-# every compiled pass variant (asw_tune_set): H block shapes (64: k_hpass9 with 10
-# waves; 128: k_hpass9 always; 4096: k_hpass11 at any size, 512: with 2-chunk
-# segments), on shapes that hit segment / row edges
-@pytest.mark.parametrize("variant", [0, 64, 128, 192, 4096, 4096 + 512])
+# the on-the-fly H pass through k_hpass9 (small frames) and through every compiled
+# tap count, edges included (image borders clamp the neighbour AND shorten dist)
+@pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35, 51])
+@pytest.mark.parametrize("scene", ["tsukuba", "ragged"])
+def test_hpass_otf_bit_exact(gpu, oracle, T, scene):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    if scene == "tsukuba":
+        Lh, Rh, _ = load_scene("tsukuba")
+        D, d0, d1 = 61, 0, 61
+    else:
+        Lh, Rh = _rand_pair(T, 37, 123)
+        D, d0, d1 = 90, 20, 90
+    H, W = Lh.shape[:2]
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
+    Dp = K.cost_shape(p)[2]
+    assert K.otf_supported(p)
+    wl, wr = K.asw_hSupport(p, _t(Lh, gpu)), K.asw_hSupport(p, _t(Rh, gpu))
+    lut, R = K.support_lut(p, gpu), _t(Rh, gpu)
+    cin = _t(pixel_major((np.random.default_rng(T).random((d1 - d0, H, W)) * 700).astype(np.float32), Dp), gpu)
+    for variant in (0, 128, 4096):  # size-selected, k_hpass9, k_hpass11
+        old = _lib.lib().asw_tune_set(1, variant)
+        try:
+            for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
+                den_a = torch.zeros(K.cost_shape(p), dtype=torch.float32, device=gpu)
+                den_b = torch.zeros(K.cost_shape(p), dtype=torch.float32, device=gpu)
+                if mode == _lib.DEN_READ:  # a real den volume to read
+                    K.asw_hCostAggregation(p, wl, wr, cin, den=den_a, den_mode=_lib.DEN_WRITE)
+                    den_b.copy_(den_a)
+                a = K.asw_hCostAggregation(p, wl, wr, cin, den=den_a, den_mode=mode)
+                b = K.asw_hCostAggregation_otf(p, wl, R, lut, cin, den=den_b, den_mode=mode)
+                assert "_otf<" in K.pass_kernel(1, mode)
+                assert torch.equal(a, b), (variant, mode)
+                assert torch.equal(den_a, den_b), (variant, mode)
+        finally:
+            _lib.lib().asw_tune_set(1, old)
+
+
+# every compiled pass variant (asw_tune_set): H block shapes (128: k_hpass9 always;
+# 4096: k_hpass11 at any size, 512: with 2-chunk segments), on shapes that hit
+# segment / row edges
+@pytest.mark.parametrize("variant", [0, 128, 4096, 4096 + 512])
 @pytest.mark.parametrize("H,W,D,d0,d1", [(9, 331, 256, 0, 256), (6, 47, 128, 0, 128), (5, 161, 300, 40, 168),
                                           (4, 400, 256, 128, 256)])
 def test_pass_variants_bit_exact(gpu, oracle, variant, H, W, D, d0, d1):
@@ -479,7 +526,8 @@ def test_c4_full_frame_oracle_parity(gpu, oracle):
     print("C4 pass kernels:", names)
     for dm in (1, 2):
         assert names[(0, dm)].startswith(f"k_vpass10<T={T},NW=16,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
-        assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW=4,DM={dm}") and names[(1, dm)].endswith(",nt>"), names
+        assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW=4,DM={dm}") and names[(1, dm)].endswith(",nt>"), \
+            names
     ref = oracle.match(Lh, Rh, D, T, 7, want_cost=True)
     for k in ("d_ref", "d_tar", "conf_ref", "conf_tar", "lr_rgba", "lr_red_rgba"):
         assert np.array_equal(_np(getattr(res, k)), ref[k]), k
@@ -489,6 +537,9 @@ def test_c4_full_frame_oracle_parity(gpu, oracle):
     assert torch.equal(res.cost, res2.cost) and torch.equal(res.d_tar, res2.d_tar)
     inner = np.s_[40:-40, 300:-40]
     assert (np.abs(_np(res.d_ref)[inner] - gt[inner]) <= 1).mean() > 0.6
+
+
+C5_H_NKW = 2  # plane blocks per k_hpass11 block at T = 51 (launch_dm)
 
 
 def test_c5_band_oracle_parity(gpu, oracle):
@@ -505,8 +556,9 @@ def test_c5_band_oracle_parity(gpu, oracle):
     names = _pass_kernels()
     print("C5 band pass kernels:", names)
     for dm in (1, 2):
-        assert names[(0, dm)].startswith(f"k_vpass10<T={T},NW=8,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
-        assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW=4,DM={dm}") and names[(1, dm)].endswith(",nt>"), names
+        assert names[(0, dm)].startswith(f"k_vpass10<T={T},NW=12,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
+        assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW={C5_H_NKW},DM={dm}") and \
+            names[(1, dm)].endswith(",nt>"), names
     ref = oracle.match(Ls, Rs, D, T, 7, want_cost=True)
     dr, dt = ref["d_ref"], ref["d_tar"]
     assert np.array_equal(_np(res.d_ref), dr) and np.array_equal(_np(res.d_tar), dt)

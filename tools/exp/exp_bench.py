@@ -23,13 +23,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--v", action="store_true", help="V-pass experiments")
+    ap.add_argument("--lib", default="libexp.so")
+    ap.add_argument("--c5", action="store_true", help="C5 block-shape experiments (T = 51)")
+    ap.add_argument("--vexps", default="prod_read,v11_read,v11_read_s3,prod_none")
     ap.add_argument("--h", action="store_true", help="H-pass experiments")
     args = ap.parse_args()
-    W, H, D, T = 1920, 1080, 256, 35
+    W, H, D, T = (3840, 2160, 512, 51) if args.c5 else (1920, 1080, 256, 35)
     dev = torch.device("cuda:0")
     Lh, Rh, _ = make_pair(W, H, D, 0)
     p = make_params(W, H, ndisp=D, taps=T, iters=7)
-    m = StereoMatcher(p, dev)
+    m = StereoMatcher(p, dev, otf=False)
     m.raw_and_support(torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev))
     # a realistic H input: one V pass of the raw cost
     cin = torch.empty_like(m.c0)
@@ -38,7 +41,7 @@ def main():
     ref = torch.empty_like(cin)
     K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=ref, den=den, den_mode=1)
     torch.cuda.synchronize()
-    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp.so"))
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", args.lib))
     pp = ctypes.byref(p)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
@@ -49,6 +52,41 @@ def main():
                          ctypes.c_void_p(st.cuda_stream))
         assert rc == 0, rc
 
+    if args.c5:
+        res = {}
+        cur = torch.cuda.current_stream().cuda_stream
+        for d, fn, wl, wr, src in ((0, K.asw_vCostAggregation, m.wvl, m.wvr, m.c0),
+                                   (1, K.asw_hCostAggregation, m.whl, m.whr, cin)):
+            den_d = torch.empty_like(cin)
+            ref_d = torch.empty_like(cin)
+            fn(p, wl, wr, src, out=ref_d, den=den_d, den_mode=1)
+            torch.cuda.synchronize()
+            print("prod", d, K.pass_kernel(d, 1), flush=True)
+            for rep in range(args.reps + 1):
+                for shape in ((8, 12) if d == 0 else (4, 2)):
+                    for kind in ("prod", "exp"):
+                        if kind == "prod" and shape != (8 if d == 0 else 4):
+                            continue
+                        out.zero_()
+                        torch.cuda.synchronize()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        if kind == "prod":
+                            fn(p, wl, wr, src, out=out, den=den_d, den_mode=2)
+                        else:
+                            assert lib.exp_c5(d, shape, 2, pp, P(wl), P(wr), P(src), P(out), P(den_d),
+                                              ctypes.c_void_p(cur)) == 0
+                        e1.record()
+                        torch.cuda.synchronize()
+                        name = f"{'vh'[d]}_{kind}_{shape}"
+                        if rep == 0:
+                            if not torch.equal(out, ref_d):
+                                print(json.dumps({"exp": name, "error": "differs"}), flush=True)
+                        else:
+                            res.setdefault(name, []).append(e0.elapsed_time(e1))
+        for name, ts in res.items():
+            print(json.dumps({"exp": name, "ms_median": round(float(np.median(ts)), 4)}), flush=True)
+        return
     # V pass experiments: the production den-write pass gives den_v, the production
     # den-read pass the reference output
     if args.v:
@@ -57,8 +95,10 @@ def main():
         K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=refv, den=denv, den_mode=1)
         torch.cuda.synchronize()
         vres = {}
-        vexps = [("prod_read", None, 2, 0), ("v11_read", 2, 2, 0), ("v11_read_s1", 2, 2, 1), ("v11_read_s3", 2, 2, 3),
-                 ("prod_none", None, 0, 0), ("v11_none", 2, 0, 0)]
+        allv = {"prod_read": (None, 2, 0), "v11_read": (2, 2, 0), "v11_read_s1": (2, 2, 1), "v11_read_s3": (2, 2, 3),
+                "v11_read_s10": (2, 2, 10), "prod_none": (None, 0, 0), "v11_none": (2, 0, 0),
+                "v10_read": (10, 2, 0), "v10dma_read": (11, 2, 0)}
+        vexps = [(n,) + allv[n] for n in args.vexps.split(",")]
         for rep in range(args.reps + 1):
             for name, kind, dm, ns in vexps:
                 out.zero_()
@@ -67,6 +107,10 @@ def main():
                 e0.record()
                 if kind is None:
                     K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=denv if dm else None, den_mode=dm)
+                elif kind in (10, 11):
+                    rc = lib.exp_v10(kind - 10, dm, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                    assert rc == 0, rc
                 else:
                     rc = lib.exp_v11(dm, ns, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))

@@ -41,24 +41,28 @@ def main():
     dev = torch.device("cuda:0")
     Lh, Rh, _ = make_pair(W, H, D, 0)
     p = make_params(W, H, ndisp=D, taps=T, iters=iters)
-    m = StereoMatcher(p, dev)
+    m = StereoMatcher(p, dev, otf=False)  # materialised whr too: both H forms are timed
     m.raw_and_support(torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev))
     torch.cuda.synchronize()
     cin = m.c0
     out = torch.empty_like(cin)
     variants = [int(v) for v in args.variants.split(",")]
     modes = [0, 1, 2] if args.den else [0]  # ASW_DEN_NONE / WRITE / READ
-    dens = {"v": torch.empty_like(cin), "h": torch.empty_like(cin)} if args.den else {}
+    dens = {"v": torch.empty_like(cin), "h": torch.empty_like(cin), "h_otf": torch.empty_like(cin)} if args.den else {}
     lib = _lib.lib()
     S = W * H
     nbytes = 8 * D * S + 8 * T * S
     ref = {}
-    times = {(v, d, dm): [] for v in variants for d in "vh" for dm in modes}
+    times = {(v, d, dm): [] for v in variants for d in ("v", "h", "h_otf") for dm in modes}
     for rep in range(args.reps + 1):
         for v in variants:
             lib.asw_tune_set(1, v)
+            right = torch.from_numpy(Rh).to(dev)
+            otf = lambda p_, wl_, wr_, cin_, out=None, den=None, den_mode=0: K.asw_hCostAggregation_otf(  # noqa: E731
+                p_, wl_, right, m.lut, cin_, out=out, den=den, den_mode=den_mode)
             for d, fn, wl, wr in (("v", K.asw_vCostAggregation, m.wvl, m.wvr),
-                                  ("h", K.asw_hCostAggregation, m.whl, m.whr)):
+                                  ("h", K.asw_hCostAggregation, m.whl, m.whr),
+                                  ("h_otf", otf, m.whl, None)):
                 for dm in modes:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
@@ -66,9 +70,10 @@ def main():
                     e1.record()
                     torch.cuda.synchronize()
                     if rep == 0:
-                        if v == variants[0] and dm == 0:
+                        key = "h" if d == "h_otf" else d
+                        if v == variants[0] and dm == 0 and d != "h_otf":
                             ref[d] = out.clone()
-                        elif not torch.equal(out, ref[d]):
+                        elif not torch.equal(out, ref[key]):
                             print(json.dumps({"variant": v, "dir": d, "den_mode": dm,
                                               "error": "output differs from variant 0"}))
                     else:
