@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--v", action="store_true", help="V-pass experiments")
     ap.add_argument("--lib", default="libexp.so")
     ap.add_argument("--c5", action="store_true", help="C5 block-shape experiments (T = 51)")
-    ap.add_argument("--vexps", default="prod_read,v11_read,v11_read_s3,prod_none")
+    ap.add_argument("--vexps", default="prod_read,v12_read,prod_none")
     ap.add_argument("--h", action="store_true", help="H-pass experiments")
     args = ap.parse_args()
     W, H, D, T = (3840, 2160, 512, 51) if args.c5 else (1920, 1080, 256, 35)
@@ -91,13 +91,14 @@ def main():
     # den-read pass the reference output
     if args.v:
         denv = torch.empty_like(cin)
+        denw = torch.empty_like(cin)
         refv = torch.empty_like(cin)
         K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=refv, den=denv, den_mode=1)
         torch.cuda.synchronize()
         vres = {}
-        allv = {"prod_read": (None, 2, 0), "v11_read": (2, 2, 0), "v11_read_s1": (2, 2, 1), "v11_read_s3": (2, 2, 3),
-                "v11_read_s10": (2, 2, 10), "prod_none": (None, 0, 0), "v11_none": (2, 0, 0),
-                "v10_read": (10, 2, 0), "v10dma_read": (11, 2, 0)}
+        allv = {"prod_read": (None, 2, 0), "prod_none": (None, 0, 0), "prod_write": (None, 1, 0),
+                "v12_read": (12, 2, 0), "v12_read_s1": (12, 2, 1), "v12_read_s3": (12, 2, 3),
+                "v12_none": (12, 0, 0), "v12_write": (12, 1, 0)}
         vexps = [(n,) + allv[n] for n in args.vexps.split(",")]
         for rep in range(args.reps + 1):
             for name, kind, dm, ns in vexps:
@@ -107,17 +108,17 @@ def main():
                 e0.record()
                 if kind is None:
                     K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=denv if dm else None, den_mode=dm)
-                elif kind in (10, 11):
-                    rc = lib.exp_v10(kind - 10, dm, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
-                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-                    assert rc == 0, rc
                 else:
-                    rc = lib.exp_v11(dm, ns, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
+                    # den-write experiments write a scratch den (compared below), never denv
+                    rc = lib.exp_v12(0, dm, ns, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out),
+                                     P(denw if dm == 1 else denv),
                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
                     assert rc == 0, rc
                 e1.record()
                 torch.cuda.synchronize()
                 if rep == 0:
+                    if dm == 1 and kind is not None and not torch.equal(denw, denv):
+                        print(json.dumps({"exp": name, "error": "den differs"}), flush=True)
                     if not torch.equal(out, refv):
                         bad = (out != refv).nonzero()
                         print(json.dumps({"exp": name, "error": "differs", "n": int(bad.shape[0]),

@@ -5,7 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include "asw_aggregate_impl.h"
-#include "asw_vpass11.h"
+#include "asw_vpass12.h"
 
 namespace asw {
 namespace agg {
@@ -21,17 +21,22 @@ extern "C" __attribute__((visibility("hidden"))) int asw_disp_pitch(const asw_pa
     return asw::round_up(asw::d_end_of_p(p) - p->d_begin, 64);
 }
 
-#ifdef EXP_V11
-extern "C" int exp_v11(int dm, int nstrip, const asw_params *p, const float *wl, const float *wr, const float *cin,
-                       float *cout, float *den, void *stream) {
+#ifdef EXP_V12
+// one k_vpass12 instantiation per build: -DV12_NW=.. -DV12_NPH=.. -DV12_PS=..
+#ifndef V12_PS
+#define V12_PS 4
+#endif
+extern "C" int exp_v12(int shape, int dm, int nstrip, const asw_params *p, const float *wl, const float *wr,
+                       const float *cin, float *cout, float *den, void *stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (p->taps != 35) return -4;
-    if (dm == 2) launch_v11<35, 12, DM_READ, 2, kCPStream>(p, wl, wr, cin, cout, den, st, nstrip);
-    else return -4;
+    if (p->taps != 35 || dm != V12_DM) return -4;
+    (void)shape;
+    launch_v12<35, V12_NW, V12_DM, 2, V12_PS, V12_NPH, kCPStream>(p, wl, wr, cin, cout, den, st, nstrip);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
 
+#ifdef EXP_C5
 // C5 (T = 51) block shapes: V columns per block, H plane blocks per block
 extern "C" int exp_c5(int dir, int shape, int dm, const asw_params *p, const float *wl, const float *wr,
                       const float *cin, float *cout, float *den, void *stream) {
@@ -50,3 +55,4 @@ extern "C" int exp_c5(int dir, int shape, int dm, const asw_params *p, const flo
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+#endif
