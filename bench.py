@@ -13,11 +13,13 @@ RGBA8 in, host maps out, as main.cpp's replacement would call it): ``value``
 stays the device-resident rate (the sum of asw_match's own HIP-event spans,
 h2d end -> consistency end), the PCIe-inclusive wall rate is reported beside it.  N > 1 GPUs (one process per GPU,
 launched by torch.distributed.run) shard the disparity axis of a frame over a
-group of G ranks with RCCL MIN all-reduces for the WTA; G = plan_groups(D, N)
-keeps >= 64 planes per rank (the pass kernels' plane block), so D=256 runs one
-frame on 2 or 4 GPUs ("scaling": "strong") and two concurrent frames, each
-d-sharded 4 ways, on 8 GPUs ("weak" from 4 to 8: the per-GPU share stays 1/4
-frame).  `value` counts every frame all groups finished.
+group of G ranks with RCCL MIN all-reduces for the WTA; G = plan_groups(D, N) is
+the smallest group >= 2 with >= 64 planes per rank (a shard repeats the frame's
+d-independent work, so the fewest shards per frame give the most maps/s: measured
+shard frames in plan_groups' doc), so D=256 runs N/2 concurrent frames, each
+d-sharded over 2 GPUs ("scaling": "weak" past N=2: the per-GPU share stays 1/2
+frame); --group-size 4 / 8 splits one frame wider (lower latency, fewer maps/s).
+`value` counts every frame all groups finished.
 
 Rank 0 prints ONE JSON line.  ``roofline`` is the dominant kernel: the V
 aggregation pass with cached denominators (k_vpass10, DEN_READ: r-1 of the 2r
@@ -80,7 +82,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--group-size", type=int, default=0,
-                    help="ranks per d-sharded frame (0: plan_groups, >= 64 planes per rank)")
+                    help="ranks per d-sharded frame (0: plan_groups, the smallest group >= 2 with >= 64 planes per rank)")
     return ap.parse_args()
 
 

@@ -168,8 +168,9 @@ def test_frame_groups_gloo(oracle, tmp_path):
 
 def test_plan_groups():
     from stereo_matchin_amd.distributed import plan_groups
-    assert [plan_groups(256, n) for n in (1, 2, 4, 8)] == [1, 2, 4, 4]
-    assert plan_groups(512, 8) == 8 and plan_groups(61, 2) == 1 and plan_groups(128, 8) == 2
+    assert [plan_groups(256, n) for n in (1, 2, 4, 8)] == [1, 2, 2, 2]
+    assert plan_groups(512, 8) == 2 and plan_groups(61, 2) == 1 and plan_groups(128, 8) == 2
+    assert plan_groups(256, 3) == 3 and plan_groups(100, 3) == 1 and plan_groups(256, 6) == 2
 
 
 def _free_port():

@@ -556,7 +556,7 @@ def test_c5_band_oracle_parity(gpu, oracle):
     names = _pass_kernels()
     print("C5 band pass kernels:", names)
     for dm in (1, 2):
-        assert names[(0, dm)].startswith(f"k_vpass10<T={T},NW=12,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
+        assert names[(0, dm)].startswith(f"k_vpass10<T={T},NW=12,NPH=3,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
         assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW={C5_H_NKW},DM={dm}") and \
             names[(1, dm)].endswith(",nt>"), names
     ref = oracle.match(Ls, Rs, D, T, 7, want_cost=True)

@@ -38,17 +38,6 @@
 namespace asw {
 namespace agg {
 
-// NPH phases over the QT = ceil(T/4) float4 tap groups: phase k = groups
-// [gb(k), gb(k+1)) = taps [tb(k), tb(k+1))
-template <int T, int NPH>
-struct Phases {
-    static constexpr int QT = (T + 3) / 4;
-    static constexpr int gb(int k) { return QT * k / NPH; }
-    static constexpr int tb(int k) { return 4 * gb(k) < T ? 4 * gb(k) : T; }
-    static constexpr int NG = (QT + NPH - 1) / NPH;  // largest phase, groups
-    static constexpr int NT = 4 * NG;                 // largest phase, taps
-};
-
 // taps [B, E) of the A and B chains, interleaved tap by tap; wl*/wr hold taps from B
 template <int U, int S, int B, int E, bool DEN, int N, int M>
 __device__ __forceinline__ void taps2(float &numA, float &denA, float &numB, float &denB, const float (&wlA)[N],

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--v", action="store_true", help="V-pass experiments")
     ap.add_argument("--lib", default="libexp.so")
     ap.add_argument("--c5", action="store_true", help="C5 block-shape experiments (T = 51)")
+    ap.add_argument("--c5libs", default="libexp_c5_1641.so:1641")
     ap.add_argument("--vexps", default="prod_read,v12_read,prod_none")
     ap.add_argument("--h", action="store_true", help="H-pass experiments")
     args = ap.parse_args()
@@ -41,7 +42,7 @@ def main():
     ref = torch.empty_like(cin)
     K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=ref, den=den, den_mode=1)
     torch.cuda.synchronize()
-    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", args.lib))
+    lib = None if args.c5 else ctypes.CDLL(os.path.join(ROOT, "tools", "exp", args.lib))
     pp = ctypes.byref(p)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
@@ -53,37 +54,37 @@ def main():
         assert rc == 0, rc
 
     if args.c5:
-        res = {}
+        # V den-read at T = 51: production pass against k_vpass10 shapes, one library each
+        # (--c5libs lib:shape,...; shape = NW*100 + NPH*10 + RB)
         cur = torch.cuda.current_stream().cuda_stream
-        for d, fn, wl, wr, src in ((0, K.asw_vCostAggregation, m.wvl, m.wvr, m.c0),
-                                   (1, K.asw_hCostAggregation, m.whl, m.whr, cin)):
-            den_d = torch.empty_like(cin)
-            ref_d = torch.empty_like(cin)
-            fn(p, wl, wr, src, out=ref_d, den=den_d, den_mode=1)
-            torch.cuda.synchronize()
-            print("prod", d, K.pass_kernel(d, 1), flush=True)
-            for rep in range(args.reps + 1):
-                for shape in ((8, 12) if d == 0 else (4, 2)):
-                    for kind in ("prod", "exp"):
-                        if kind == "prod" and shape != (8 if d == 0 else 4):
-                            continue
-                        out.zero_()
-                        torch.cuda.synchronize()
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0.record()
-                        if kind == "prod":
-                            fn(p, wl, wr, src, out=out, den=den_d, den_mode=2)
-                        else:
-                            assert lib.exp_c5(d, shape, 2, pp, P(wl), P(wr), P(src), P(out), P(den_d),
-                                              ctypes.c_void_p(cur)) == 0
-                        e1.record()
-                        torch.cuda.synchronize()
-                        name = f"{'vh'[d]}_{kind}_{shape}"
-                        if rep == 0:
-                            if not torch.equal(out, ref_d):
-                                print(json.dumps({"exp": name, "error": "differs"}), flush=True)
-                        else:
-                            res.setdefault(name, []).append(e0.elapsed_time(e1))
+        exps = [(lb, int(sh)) for lb, sh in (x.split(":") for x in args.c5libs.split(","))]
+        libs = {lb: ctypes.CDLL(os.path.join(ROOT, "tools", "exp", lb)) for lb, _ in exps}
+        den_d = torch.empty_like(cin)
+        ref_d = torch.empty_like(cin)
+        K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=ref_d, den=den_d, den_mode=1)
+        K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=ref_d, den=den_d, den_mode=2)
+        torch.cuda.synchronize()
+        print("prod", K.pass_kernel(0, 2), flush=True)
+        res = {}
+        for rep in range(args.reps + 1):
+            for lb, sh in [(None, 0)] + exps:
+                out.zero_()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                if lb is None:
+                    K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=den_d, den_mode=2)
+                else:
+                    assert libs[lb].exp_c5(0, sh, 2, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(den_d),
+                                           ctypes.c_void_p(cur)) == 0
+                e1.record()
+                torch.cuda.synchronize()
+                name = f"v_read_{sh or 'prod'}"
+                if rep == 0:
+                    if not torch.equal(out, ref_d):
+                        print(json.dumps({"exp": name, "error": "differs"}), flush=True)
+                else:
+                    res.setdefault(name, []).append(e0.elapsed_time(e1))
         for name, ts in res.items():
             print(json.dumps({"exp": name, "ms_median": round(float(np.median(ts)), 4)}), flush=True)
         return

@@ -37,22 +37,16 @@ extern "C" int exp_v12(int shape, int dm, int nstrip, const asw_params *p, const
 #endif
 
 #ifdef EXP_C5
-// C5 (T = 51) block shapes: V columns per block, H plane blocks per block
+// C5 (T = 51) V shapes: shape = NW * 100 + NPH * 10 + RB (PS = 2 when RB = 1, else 4)
 extern "C" int exp_c5(int dir, int shape, int dm, const asw_params *p, const float *wl, const float *wr,
                       const float *cin, float *cout, float *den, void *stream) {
     hipStream_t st = (hipStream_t)stream;
-    if (p->taps != 51 || dm != 2) return -4;
-    if (dir == 0) {
-        if (shape == 8) launch_v10<51, 8, DM_READ, 2, kCPStream>(p, wl, wr, cin, cout, den, st);
-        else if (shape == 12) launch_v10<51, 12, DM_READ, 2, kCPStream>(p, wl, wr, cin, cout, den, st);
-        else return -4;
-    } else {
-        constexpr int U = pf9_period(51);
-        const int seg = (240 + U / 2) / U * U;
-        if (shape == 4) launch_h11<51, 4, DM_READ, kCPStream>(p, wl, wr, cin, cout, den, st, seg);
-        else if (shape == 2) launch_h11<51, 2, DM_READ, kCPStream>(p, wl, wr, cin, cout, den, st, seg);
-        else return -4;
-    }
+    if (p->taps != 51 || dm != 2 || dir != 0) return -4;
+    if (shape == C5_NW * 100 + C5_NPH * 10 + C5_RB)
+        launch_v10<51, C5_NW, DM_READ, C5_RB, kCPStream, kCPStream, C5_RB == 1 ? 2 : 4, C5_NPH>(p, wl, wr, cin, cout,
+                                                                                               den, st);
+    else
+        return -4;
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
