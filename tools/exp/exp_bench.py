@@ -42,7 +42,7 @@ def main():
     ref = torch.empty_like(cin)
     K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=ref, den=den, den_mode=1)
     torch.cuda.synchronize()
-    lib = None if args.c5 else ctypes.CDLL(os.path.join(ROOT, "tools", "exp", args.lib))
+    lib = None if args.c5 or args.lib == "none" else ctypes.CDLL(os.path.join(ROOT, "tools", "exp", args.lib))
     pp = ctypes.byref(p)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
@@ -97,9 +97,11 @@ def main():
         K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=refv, den=denv, den_mode=1)
         torch.cuda.synchronize()
         vres = {}
+        pxlibs = {}
         allv = {"prod_read": (None, 2, 0), "prod_none": (None, 0, 0), "prod_write": (None, 1, 0),
                 "v12_read": (12, 2, 0), "v12_read_s1": (12, 2, 1), "v12_read_s3": (12, 2, 3),
-                "v12_none": (12, 0, 0), "v12_write": (12, 1, 0)}
+                "v12_none": (12, 0, 0), "v12_write": (12, 1, 0),
+                "vpx0": ("px0", 2, 0), "vpx4": ("px4", 2, 0), "vpx8": ("px8", 2, 0)}
         vexps = [(n,) + allv[n] for n in args.vexps.split(",")]
         for rep in range(args.reps + 1):
             for name, kind, dm, ns in vexps:
@@ -109,6 +111,11 @@ def main():
                 e0.record()
                 if kind is None:
                     K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=denv if dm else None, den_mode=dm)
+                elif isinstance(kind, str):  # k_vpass10 with extra cost prefetch (libexp_vpx<N>.so)
+                    lx = pxlibs.setdefault(kind, ctypes.CDLL(os.path.join(ROOT, "tools", "exp", f"libexp_v{kind}.so")))
+                    rc = lx.exp_vpx(dm, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
+                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                    assert rc == 0, rc
                 else:
                     # den-write experiments write a scratch den (compared below), never denv
                     rc = lib.exp_v12(0, dm, ns, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out),
