@@ -52,22 +52,30 @@ extern "C" int exp_c5(int dir, int shape, int dm, const asw_params *p, const flo
 #endif
 
 #ifdef EXP_VPX
-// k_vpass10 at T = 35 with PX extra cost-prefetch steps (window U = 40 + PX)
+// k_vpass10 at T = 35, den-read: block shape / occupancy experiments
+//   -DEXP_VPX=<extra prefetch> -DVNW=<columns> -DVNPH=<phases> -DVRB=<rows per barrier> -DVPS=<staging rows> -DVWPE=<waves/EU>
+#ifndef VNW
+#define VNW 16
+#define VNPH 2
+#define VRB 2
+#define VPS 4
+#define VWPE 0
+#endif
 extern "C" int exp_vpx(int dm, const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
                        float *den, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     if (p->taps != 35 || dm != 2) return -4;
     constexpr int U = pf9_period(35) + EXP_VPX;
-    const int W = p->width, H = p->height, Dp = asw_disp_pitch(p), nkb = Dp / 64, nxb = (W + 15) / 16;
+    const int W = p->width, H = p->height, Dp = asw_disp_pitch(p), nkb = Dp / 64, nxb = (W + VNW - 1) / VNW;
     int nstrip = (int)((2048LL + (long long)nxb * nkb - 1) / ((long long)nxb * nkb));
     const int max_strip = H / 70 > 1 ? H / 70 : 1;
     if (nstrip > max_strip) nstrip = max_strip;
     const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
     nstrip = (H + rows - 1) / rows;
     const int per_xcd = (nxb + 7) / 8;
-    hipLaunchKernelGGL((k_vpass10<35, 16, DM_READ, 2, kCPStream, kCPStream, 2, 4, false, 2, EXP_VPX>),
-                       dim3(8 * per_xcd * nkb * nstrip), dim3(1024), 0, st, wl, wr, cin, cout, den, W, H, Dp, p->d_begin,
-                       rows, nxb, nstrip, per_xcd);
+    hipLaunchKernelGGL((k_vpass10<35, VNW, DM_READ, VRB, kCPStream, kCPStream, 2, VPS, false, VNPH, EXP_VPX, VWPE>),
+                       dim3(8 * per_xcd * nkb * nstrip), dim3(VNW * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp,
+                       p->d_begin, rows, nxb, nstrip, per_xcd);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
