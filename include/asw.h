@@ -299,9 +299,7 @@ typedef struct asw_outputs { /* caller-owned host arrays; any may be NULL */
 } asw_outputs;
 #define ASW_DISP16_INVALID 0xFFFF
 
-typedef struct asw_timings { /* milliseconds from HIP events, columns of main.cpp:181;
-                                 raw_cost and support overlap on two streams: support is the
-                                 part of the support stage not hidden under the raw cost */
+typedef struct asw_timings { /* milliseconds from HIP events, columns of main.cpp:181 */
     double raw_cost, support, v_pass_mean, h_pass_mean, aggregation_total, wta, consistency, total;
     double h2d, d2h;
     double refine;           /* refinement loop + median (0 when off) */

@@ -32,8 +32,6 @@ enum CommMode { COMM_NONE = 0, COMM_RCCL = 1, COMM_LOCAL = 2 };
 struct Shard {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;                    // asw_raw_cost, overlapped with the supports
-    hipEvent_t fork = nullptr, join = nullptr;     // stream -> side -> stream
     asw_params p{};                     // this shard's [d_begin, d_end)
     uint8_t *left = nullptr, *right = nullptr;  // RGBA8 [H][W][4]
     float *lut = nullptr;
@@ -242,9 +240,6 @@ void free_shard(Shard &s) {
         if (b) (void)hipFree(b);
     if (s.comm) (void)ncclCommDestroy(s.comm);
     if (s.ready) (void)hipEventDestroy(s.ready);
-    if (s.fork) (void)hipEventDestroy(s.fork);
-    if (s.join) (void)hipEventDestroy(s.join);
-    if (s.side) (void)hipStreamDestroy(s.side);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Shard{};
 }
@@ -254,10 +249,7 @@ int alloc_shard(Shard &s, bool sharded) {
     const size_t S = frame_pixels(p);
     HIPCHK(hipSetDevice(s.device));
     HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&s.ready, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&s.fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&s.join, hipEventDisableTiming));
     ASWCHK(dev_alloc(&s.left, S * 4));
     ASWCHK(dev_alloc(&s.right, S * 4));
     ASWCHK(dev_alloc(&s.lut, asw_lut_bytes(p)));
@@ -425,15 +417,9 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
     if (timed) HIPCHK(hipEventRecord(c->ev[e_raw], st));
     // the raw cost volume and the first V pass as two kernels: fusing asw_Aggr into
     // that pass (asw_aggregate_pass_raw) is bit-identical but measured slower on
-    // MI355X (3.10 ms vs 0.64 + 2.02 ms at C4, profiles/r01/kernel_stats_fused_raw.csv).
-    // asw_Aggr (bandwidth-bound stores) runs on the side stream while the
-    // latency-bound support kernel runs here; the passes wait for both (so
-    // asw_timings.support is the support time NOT hidden under the raw cost)
-    HIPCHK(hipEventRecord(s.fork, st));
-    HIPCHK(hipStreamWaitEvent(s.side, s.fork, 0));
-    ASWCHK(asw_raw_cost(p, s.left, s.right, s.c0, s.side));
-    if (timed) HIPCHK(hipEventRecord(c->ev[e_raw + 1], s.side));
-    HIPCHK(hipEventRecord(s.join, s.side));
+    // MI355X (3.10 ms vs 0.64 + 2.02 ms at C4, profiles/r01/kernel_stats_fused_raw.csv)
+    ASWCHK(asw_raw_cost(p, s.left, s.right, s.c0, st));
+    if (timed) HIPCHK(hipEventRecord(c->ev[e_raw + 1], st));
     if (p->color_space == ASW_COLOR_LAB) {
         ASWCHK(asw_lab(p, s.left, s.lab_l, st));
         ASWCHK(asw_lab(p, s.right, s.lab_r, st));
@@ -445,7 +431,6 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         ASWCHK(asw_support_lut(p, s.lut, st));
         ASWCHK(asw_support_all(p, s.left, s.right, s.lut, s.wvl, s.whl, s.wvr, s.otf ? nullptr : s.whr, st));
     }
-    HIPCHK(hipStreamWaitEvent(st, s.join, 0));
     if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0], st));
     for (int it = 0; it < p->iters; ++it) {
         const int dm = !s.den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);

@@ -12,8 +12,6 @@ CLI path.
 """
 from __future__ import annotations
 
-import os
-
 import ctypes
 from dataclasses import dataclass
 
@@ -43,10 +41,6 @@ class MatchResult:
     cost: torch.Tensor        # final aggregated volume [H][W][Dp]
 
 
-# ASW_SERIAL_RAW=1: asw_Aggr and the supports back to back on one stream (A/B of the overlap)
-_SERIAL_RAW = os.environ.get("ASW_SERIAL_RAW") == "1"
-
-
 class StereoMatcher:
     """One GPU, one disparity shard: the buffers of main.cpp:434-457, allocated once.
 
@@ -72,7 +66,6 @@ class StereoMatcher:
         # registers cost the pass its latency cover; DESIGN.md §On-the-fly supports)
         self.otf = False if otf is None else (otf and K.otf_supported(self.p))
         self.right = None
-        self._side = None  # side stream of asw_Aggr (raw_and_support)
         self.wvl = K.new_support(self.p, dev)
         self.wvr = K.new_support(self.p, dev)
         self.whl = K.new_support(self.p, dev)
@@ -89,26 +82,8 @@ class StereoMatcher:
         """asw_Aggr into c0 (unless ``raw`` is False: the first V pass computes it,
         see ``aggregate(images=...)``) and the four support arrays."""
         p = self.p
-        if raw and _SERIAL_RAW:
-            K.asw_Aggr(p, left, right, out=self.c0)
-            raw = False
         if raw:
-            # asw_Aggr (bandwidth-bound: 2.1 GB of stores at C4) on a side stream, so
-            # the latency-bound support kernel overlaps it; joined below
-            cur = torch.cuda.current_stream(self.device)
-            if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
-            self._side.wait_stream(cur)
-            with torch.cuda.stream(self._side):
-                K.asw_Aggr(p, left, right, out=self.c0)
-        try:
-            self._supports(left, right)
-        finally:
-            if raw:
-                cur.wait_stream(self._side)
-
-    def _supports(self, left: torch.Tensor, right: torch.Tensor):
-        p = self.p
+            K.asw_Aggr(p, left, right, out=self.c0)
         if p.color_space == COLOR_LAB:
             lab_l, lab_r = K.lab_image(p, left), K.lab_image(p, right)
             K.support_lab(p, DIR_V, lab_l, out=self.wvl)
