@@ -151,11 +151,15 @@ def _group_worker(rank, world, G, port, D, H, W, out_dir):
         dist.destroy_process_group()
 
 
-def test_frame_groups_gloo(oracle, tmp_path):
+@pytest.mark.parametrize("world,G", [(4, 0), (8, 0), (8, 8)])
+def test_frame_groups_gloo(oracle, tmp_path, world, G):
+    """bench.py --gpus 4 / 8 layouts on gloo: plan_groups' 2-way groups (G = 0), and one
+    frame d-sharded 8 ways (--group-size 8)."""
     from stereo_matchin_amd.distributed import plan_groups
-    world, D, H, W = 4, 16, 4, 18
-    G = plan_groups(D, world, min_planes=8)
-    assert G == 2
+    D, H, W = 16, 4, 18
+    if not G:
+        G = plan_groups(D, world, min_planes=8)
+        assert G == 2
     mp.start_processes(_group_worker, args=(world, G, _free_port(), D, H, W, str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")
     for gid in range(world // G):
@@ -179,7 +183,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,D,H,W", [(2, 16, 6, 20), (3, 13, 5, 17), (2, 61, 4, 70)])
+@pytest.mark.parametrize("world,D,H,W", [(2, 16, 6, 20), (3, 13, 5, 17), (2, 61, 4, 70), (8, 64, 4, 40)])
 def test_sharded_wta_gloo_matches_oracle(oracle, tmp_path, world, D, H, W):
     seed = 1234 + world + D
     out = str(tmp_path / "res.npz")
