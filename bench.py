@@ -111,6 +111,7 @@ def cpu_baseline(Lh, Rh, D, T, iters, rows, lr_mode):
         return time.perf_counter() - t0
 
     threads = O.set_threads(0)
+    aff = sorted(os.sched_getaffinity(0))
     rows = min(rows, H)
     dt = timed(rows)
     what = "the full frame" if rows == H else f"a {Lh.shape[1]}x{rows} strip (rows 0-{rows - 1}), scaled x{H}/{rows}"
@@ -133,36 +134,54 @@ def cpu_baseline(Lh, Rh, D, T, iters, rows, lr_mode):
         "sample": f"{what}: full pipeline r={iters} (raw cost, supports, 2r passes, WTA + target, LR check), "
                   f"{dt:.3f} s measured, {frame_s * 1000:.1f} ms/map",
         "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+        # where `cores` comes from: OpenMP's default team = OMP_NUM_THREADS (the GPU box's job
+        # environment sets 16), run inside this process's CPU affinity mask
+        "threads_source": f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', '(unset: every CPU of the mask)')}",
+        "affinity_cpus": len(aff), "affinity_mask": _ranges(aff),
         "one_thread": {"value": round(1.0 / one_s, 6), "unit": "maps/s",
                        "sample": f"{Lh.shape[1]}x{r1} strip, median of 3 runs ({t1:.2f} s), scaled x{H}/{r1}; "
                                  f"{one_s * 1000:.0f} ms/map"},
     }
 
 
-def h_kernel_name(W, H, nloc, T, otf=False):
-    """The H pass kernel launch_dm (asw_aggregate_impl.h) selects for this shape: k_hpass11
-    when its row-segment grid has >= 8192 waves, else k_hpass9 (_otf: right weights
-    computed on the fly)."""
-    U = T + 3
-    while U % 4:
-        U += 1
-    seg = (240 + U // 2) // U * U
-    nkb = (nloc + 63) // 64
-    waves = H * ((W + seg - 1) // seg) * nkb
-    sfx = "_otf" if otf else ""
-    return f"k_hpass11{sfx}<DM_READ>" if waves >= 8192 else f"k_hpass9{sfx}<DM_READ>"
+def _ranges(cpus):
+    """[0, 1, 2, 5] -> "0-2,5" (a CPU affinity mask)."""
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
 
 
-def load_traffic(path, workload, n_gpus, kernel):
-    """Per-launch HBM bytes of `kernel` from profiles/traffic.json (rocprofv3 PMC)."""
+def ran_kernel(direction):
+    """The instantiation the library last launched for (direction, DEN_READ) in this process
+    (asw_pass_kernel, e.g. "k_hpass11<T=35,NKW=4,DM=2,nt>"), and its traffic.json keys:
+    "<kernel><T=..,DM_READ>" then the older "<kernel><DM_READ>"."""
+    from stereo_matchin_amd import _lib
+    from stereo_matchin_amd import kernels as K
+    full = K.pass_kernel(direction, _lib.DEN_READ) or "unknown<>"
+    base = full.split("<")[0]
+    taps = [a for a in full[len(base) + 1:-1].split(",") if a.startswith("T=")]
+    keys = ([f"{base}<{taps[0]},DM_READ>"] if taps else []) + [f"{base}<DM_READ>"]
+    return full, keys
+
+
+def load_traffic(path, workload, n_gpus, keys):
+    """Per-launch HBM bytes of the kernel (first of `keys` present) from profiles/traffic.json
+    (rocprofv3 PMC)."""
     try:
         with open(path) as f:
             t = json.load(f)
         e = t.get(f"{workload}_n{n_gpus}") or {}
-        k = e.get(kernel) or {}
-        return k.get("total_bytes")
+        for k in keys:
+            if k in e:
+                return e[k].get("total_bytes")
     except (OSError, ValueError):
-        return None
+        pass
+    return None
 
 
 def load_pairs(workload, W, H, D, n):
@@ -351,7 +370,7 @@ def main():
         maps_per_s = n_maps / (span_sum / 1e3) if frame else n_maps / elapsed
         dom = "v" if (v_avg >= h_avg or h_avg != h_avg) else "h"
         dom_ms = v_avg if dom == "v" else h_avg
-        kname = "k_vpass10<DM_READ>" if dom == "v" else h_kernel_name(W, H, nloc, T, getattr(getattr(m, "matcher", m), "otf", False))
+        kname, tkeys = ran_kernel(0 if dom == "v" else 1)
         out = {
             "metric": METRIC,
             "value": round(maps_per_s, 4),
@@ -375,7 +394,7 @@ def main():
                                        if world > 1 else "single GPU")},
             "roofline": {"bound": "hbm", "achieved": round(gbs(dom_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs(dom_ms) / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(args.traffic, args.workload, world, kname),
+                         "traffic": load_traffic(args.traffic, args.workload, world, tkeys),
                          "kernel": f"{kname}: {'V' if dom == 'v' else 'H'} aggregation pass reading cached "
                                    f"denominators ({max(iters - 1, 0)} of the {2 * iters} launches per frame)",
                          "bytes_per_launch": bytes_per_pass, "avg_launch_ms": round(dom_ms, 4),

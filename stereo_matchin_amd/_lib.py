@@ -31,6 +31,9 @@ ASW_E_UNSUPPORTED = -4
 ASW_E_COMM = -5
 DISP16_INVALID = 0xFFFF
 COMM_ID_BYTES = 128
+# the asw_outputs / asw_timings layouts mirrored below (ASW_ABI_VERSION of include/asw.h):
+# a library of another revision would write past them, so _load() refuses it
+ABI_VERSION = 2
 
 DIR_V = 0
 DIR_H = 1
@@ -198,6 +201,12 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    got = L.asw_abi_version()
+    if got != ABI_VERSION:
+        _load_error = AswLibraryError(
+            f"{LIB_PATH} has ABI revision {got}, this binding mirrors revision {ABI_VERSION} "
+            "(asw_outputs / asw_timings layouts differ): rebuild the library")
+        raise _load_error
     _lib = L
     return L
 

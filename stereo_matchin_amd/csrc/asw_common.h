@@ -54,6 +54,9 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
 // raw-cost pass support)
 bool ring_taps(int T);
 int set_pass_variant(int v);
+// the asw_tune_set(ASW_TUNE_PASS_VARIANT) bits launch_dm reads: 128 = H by k_hpass9,
+// 4096 = H by k_hpass11 at any size, 0xF00 = k_hpass11 segment length in U-step chunks
+constexpr int kPassVariantBits = 128 | 4096 | 0xF00;
 // records the instantiation a pass launch of (dir, dm) runs (asw_pass_kernel)
 void note_pass_kernel(int dir, int dm, const char *kernel, int T, const char *shape, bool nt);
 // ASW_OK when the pass kernels can address a (shard) context of this shape: they use

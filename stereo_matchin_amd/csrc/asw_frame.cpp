@@ -363,15 +363,15 @@ int create_ctx(const asw_params *p, const int *devs, int n, int shard0, int tota
     }
     if (s == ASW_OK && comm == COMM_RCCL) {
         ncclComm_t comms[kMaxShards] = {};
-        ncclResult_t r;
+        ncclResult_t r = ncclSuccess;
         if (id) {  // one process per GPU
             const hipError_t e = hipSetDevice(devs[0]);
-            r = e == hipSuccess ? ncclCommInitRank(&comms[0], total, *id, shard0) : ncclInvalidUsage;
-            if (e != hipSuccess) asw::set_hip_error(e);
+            if (e != hipSuccess) s = hip_fail(e);  // a device-selection failure, not a communicator one
+            else r = ncclCommInitRank(&comms[0], total, *id, shard0);
         } else {
             r = ncclCommInitAll(comms, n, devs);
         }
-        if (r != ncclSuccess) s = ASW_E_COMM;
+        if (s == ASW_OK && r != ncclSuccess) s = ASW_E_COMM;
         for (int i = 0; i < n; ++i) c->sh[i].comm = comms[i];
     }
     if (s == ASW_OK) {

@@ -585,8 +585,14 @@ int asw_abi_version(void) { return ASW_ABI_VERSION; }
 static int g_wta_variant = 0;
 
 int asw_tune_set(int key, int value) {
-    if (key == ASW_TUNE_PASS_VARIANT) return asw::set_pass_variant(value);
+    if (key == ASW_TUNE_PASS_VARIANT) {
+        // only bits that select a compiled form (launch_dm): a stale bit would time the
+        // default kernel under another name
+        if (value & ~asw::kPassVariantBits) return ASW_E_INVALID;
+        return asw::set_pass_variant(value);
+    }
     if (key == ASW_TUNE_WTA_VARIANT) {
+        if (value != 0 && value != 1) return ASW_E_INVALID;
         const int old = g_wta_variant;
         g_wta_variant = value;
         return old;

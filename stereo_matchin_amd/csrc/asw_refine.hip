@@ -23,9 +23,6 @@
 namespace asw {
 namespace {
 
-#ifndef ASW_WTA_PROBE
-#define ASW_WTA_PROBE 0
-#endif
 constexpr float kSentinel = 100000.0f;  // K/asw_wta.cl:25-26, K/asw_wta_ref.cl:20-21
 constexpr int kChunk = 32;              // planes per transposed chunk
 constexpr int kTilePitch = kChunk + 1;
@@ -170,18 +167,12 @@ __device__ __forceinline__ void target_scan_skewed(const float *__restrict__ cos
         float tv[kGather];
 #pragma unroll
         for (int k = 0; k < kGather; ++k) {
-#if ASW_WTA_PROBE == 1  // diagnostic builds only (results WRONG): one coalesced 256-B read per step
-            tv[k] = bload(rsc, lane * 4 + ((j + k) & 1023) * 1024);
-#elif ASW_WTA_PROBE == 2  // no target gathers at all
-            tv[k] = (float)(j + k);
-#else
             // only lanes inside their interval issue the gather (exec-masked): the
             // address unit then serves fewer lanes, 0.634 -> 0.612 ms at C4
             // (profiles/r03/wta_probe_r08j.log); the others keep +inf
             const int i = j + k - skew;
             tv[k] = __builtin_inff();
             if ((unsigned)(i - i_lo) < (unsigned)ilen) tv[k] = bload(rsc, max(A - (j + k) * stride, flo));
-#endif
         }
 #pragma unroll
         for (int k = 0; k < kGather; ++k) {

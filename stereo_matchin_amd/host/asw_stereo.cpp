@@ -131,6 +131,11 @@ int main(int argc, char **argv) {
         usage();
         return 2;
     }
+    if (asw_abi_version() != ASW_ABI_VERSION) {  // asw_outputs / asw_timings layouts (include/asw.h)
+        std::fprintf(stderr, "libasw_hip.so has ABI revision %d, asw_stereo was built for %d: rebuild\n",
+                     asw_abi_version(), ASW_ABI_VERSION);
+        return 1;
+    }
     if (o.root.empty()) o.root = dir_of(o.pics);
     std::vector<std::string> lefts, rights;
     if (!read_pairs(o.pics, lefts, rights)) {

@@ -65,7 +65,10 @@ class StereoMatcher:
         # but measured slower (C4 H den-read 2.30 against 1.42 ms: the refill pipeline's
         # registers cost the pass its latency cover; DESIGN.md §On-the-fly supports)
         self.otf = False if otf is None else (otf and K.otf_supported(self.p))
-        self.right = None
+        # otf: a matcher-owned copy of the right image (the H passes read it after
+        # raw_and_support returns; the caller's buffer may be reused by then)
+        self.right = torch.empty((self.p.height, self.p.width, 4), dtype=torch.uint8, device=dev) \
+            if self.otf else None
         self.wvl = K.new_support(self.p, dev)
         self.wvr = K.new_support(self.p, dev)
         self.whl = K.new_support(self.p, dev)
@@ -95,7 +98,8 @@ class StereoMatcher:
         # asw_vSupport / asw_hSupport of both images (main.cpp:469-484) in one launch
         # (without asw_hSupport(right) when the H passes compute it on the fly)
         K.support_all(p, left, right, self.lut, self.wvl, self.whl, self.wvr, self.whr)
-        self.right = right
+        if self.otf:
+            self.right.copy_(right.reshape(self.right.shape))
 
     def aggregate(self, events: list | None = None, images: tuple | None = None):
         """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515).

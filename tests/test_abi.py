@@ -26,7 +26,20 @@ def test_every_header_symbol_is_exported(L):
 
 
 def test_abi_version(L):
+    import re
     assert L.lib().asw_abi_version() == 2
+    # the binding's mirrored struct layouts are the header's revision (_load refuses others)
+    hdr = open(os.path.join(ROOT, "include", "asw.h")).read()
+    assert int(re.search(r"#define ASW_ABI_VERSION (\d+)", hdr).group(1)) == L.ABI_VERSION
+
+
+def test_tune_set_rejects_bits_that_select_nothing(L):
+    lib = L.lib()
+    assert lib.asw_tune_set(1, 64) == L.ASW_E_INVALID      # round 1's 10-wave H form: no longer built
+    assert lib.asw_tune_set(1, 1 << 20) == L.ASW_E_INVALID
+    assert lib.asw_tune_set(2, 5) == L.ASW_E_INVALID
+    old = lib.asw_tune_set(1, 128)
+    assert lib.asw_tune_set(1, old) == 128
 
 
 def test_default_params_are_the_reference_values(L):

@@ -25,14 +25,15 @@ DM = {0: "DM_NONE", 1: "DM_WRITE", 2: "DM_READ"}
 
 
 def key_of(name: str):
-    """k_vpass10<35, 16, 2, ...> -> k_vpass10<DM_READ>; k_hpass9<35, 4, 40, 2> -> k_hpass9<DM_READ>;
-    k_hpass11<35, 4, 2, ...> -> k_hpass11<DM_READ> (template argument order of each kernel)."""
-    m = re.match(r"(k_vpass10|k_vpass9|k_hpass9|k_hpass11)<([^>]*)>", name)
+    """k_vpass10<35, 16, 2, ...> -> k_vpass10<T=35,DM_READ>; k_hpass9<35, 4, 40, 2> ->
+    k_hpass9<T=35,DM_READ>; k_hpass11<35, 4, 2, ...> -> k_hpass11<T=35,DM_READ> (template
+    argument order of each kernel; bench.py looks the kernel asw_pass_kernel names up this way)."""
+    m = re.match(r"(k_vpass10|k_vpass9|k_hpass9|k_hpass11|k_vpass32|k_hpass32)<([^>]*)>", name)
     if not m:
         return None
     args = [a.strip() for a in m.group(2).split(",")]
     dm = int(args[3]) if m.group(1) == "k_hpass9" else int(args[2])
-    return f"{m.group(1)}<{DM[dm]}>"
+    return f"{m.group(1)}<T={args[0]},{DM[dm]}>"
 
 
 def main():

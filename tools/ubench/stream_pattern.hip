@@ -11,6 +11,12 @@
 //   v4x4      V: block = 4 columns x all 4 plane blocks (1 KB contiguous per column)
 //   v8x2      V: block = 8 columns x 2 plane blocks
 //   h4        H: block = the 4 plane blocks of one pixel row segment (k_hpass11), 240 columns
+// Access width: the patterns above move 4 B per lane per
+// instruction, as the passes do.  flat_w8 / flat_w16 and h_w8 / h_w16 are the same
+// streams with 8- and 16-byte loads and stores per lane (float2 / float4: a wave covers
+// 128 / 256 consecutive planes), flat_*_pf16 with 16 accesses in flight per wave, and
+// *_def the default cache policy instead of nt: whether the 4-B access width, not the
+// machine, sets the ~5.2 TB/s of the 3-stream pattern.
 // Build: hipcc --offload-arch=gfx950 -O3 -o stream_pattern stream_pattern.hip
 #include <hip/hip_runtime.h>
 
@@ -42,6 +48,72 @@ __global__ __launch_bounds__(1024) void k_flat(const float *a, const float *b, f
             const long long cc = c + k * nw;
             if (cc < chunks) st(o + cc * 64 + lane, x[k] * y[k]);
         }
+    }
+}
+
+// flat streams with VW floats per lane and access (VW = 2: float2, 4: float4), PFW
+// accesses of each input in flight per wave; NT = nontemporal loads / stores
+template <int VW, int PFW, bool NT>
+__global__ __launch_bounds__(1024) void k_flat_w(const float *a, const float *b, float *o, long long n) {
+    using v_t = float __attribute__((ext_vector_type(VW)));
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    const long long chunks = n / (64 * VW);
+    const v_t *av = reinterpret_cast<const v_t *>(a), *bv = reinterpret_cast<const v_t *>(b);
+    v_t *ov = reinterpret_cast<v_t *>(o);
+    for (long long c = wave; c < chunks; c += nw * PFW) {
+        v_t x[PFW], y[PFW];
+#pragma unroll
+        for (int k = 0; k < PFW; ++k) {
+            const long long cc = c + k * nw;
+            if (cc < chunks) {
+                if constexpr (NT) {
+                    x[k] = __builtin_nontemporal_load(av + cc * 64 + lane);
+                    y[k] = __builtin_nontemporal_load(bv + cc * 64 + lane);
+                } else {
+                    x[k] = av[cc * 64 + lane];
+                    y[k] = bv[cc * 64 + lane];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PFW; ++k) {
+            const long long cc = c + k * nw;
+            if (cc < chunks) {
+                if constexpr (NT) __builtin_nontemporal_store(x[k] * y[k], ov + cc * 64 + lane);
+                else ov[cc * 64 + lane] = x[k] * y[k];
+            }
+        }
+    }
+}
+
+// H pattern with VW planes per lane: a wave covers 64*VW planes of one pixel, the
+// block the Dp/(64 VW) waves of one row segment
+template <int VW>
+__global__ __launch_bounds__(256) void k_h_w(const float *a, const float *b, float *o, int nseg, int seg,
+                                             int per_xcd) {
+    using v_t = float __attribute__((ext_vector_type(VW)));
+    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int g = xcd * per_xcd + m;
+    if (m >= per_xcd || g >= H * nseg) return;
+    const int y = g / nseg, xs = (g % nseg) * seg, xe = min(W, xs + seg);
+    const int lane = threadIdx.x & 63, kb = threadIdx.x >> 6;
+    const long long base = ((long long)y * W * Dp + kb * 64 * VW) / VW + lane;  // in v_t units
+    const v_t *av = reinterpret_cast<const v_t *>(a), *bv = reinterpret_cast<const v_t *>(b);
+    v_t *ov = reinterpret_cast<v_t *>(o);
+    constexpr int XS = Dp / VW;  // v_t per column
+    for (int x = xs; x < xe; x += PF) {
+        v_t u[PF], v[PF];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const long long i = base + (long long)min(x + k, W - 1) * XS;
+            u[k] = __builtin_nontemporal_load(av + i);
+            v[k] = __builtin_nontemporal_load(bv + i);
+        }
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if (x + k < xe) __builtin_nontemporal_store(u[k] * v[k], ov + base + (long long)(x + k) * XS);
     }
 }
 
@@ -154,6 +226,21 @@ int main() {
     {
         const int seg = 240, nseg = (W + seg - 1) / seg, per_xcd = (H * nseg + 7) / 8;
         time("h4_seg240", [&] { hipLaunchKernelGGL(k_h, dim3(8 * per_xcd), dim3(256), 0, 0, a, b, o, nseg, seg, per_xcd); });
+        time("h_w8_seg240", [&] {
+            hipLaunchKernelGGL(k_h_w<2>, dim3(8 * per_xcd), dim3(128), 0, 0, a, b, o, nseg, seg, per_xcd);
+        });
+        time("h_w16_seg240", [&] {
+            hipLaunchKernelGGL(k_h_w<4>, dim3(8 * per_xcd), dim3(64), 0, 0, a, b, o, nseg, seg, per_xcd);
+        });
     }
+    time("flat_w4_pf8_def", [&] { hipLaunchKernelGGL((k_flat_w<1, 8, false>), dim3(4096), dim3(1024), 0, 0, a, b, o, n); });
+    time("flat_w4_pf16", [&] { hipLaunchKernelGGL((k_flat_w<1, 16, true>), dim3(4096), dim3(1024), 0, 0, a, b, o, n); });
+    time("flat_w8", [&] { hipLaunchKernelGGL((k_flat_w<2, 8, true>), dim3(4096), dim3(1024), 0, 0, a, b, o, n); });
+    time("flat_w8_def", [&] { hipLaunchKernelGGL((k_flat_w<2, 8, false>), dim3(4096), dim3(1024), 0, 0, a, b, o, n); });
+    time("flat_w16", [&] { hipLaunchKernelGGL((k_flat_w<4, 4, true>), dim3(4096), dim3(1024), 0, 0, a, b, o, n); });
+    time("flat_w16_pf8", [&] { hipLaunchKernelGGL((k_flat_w<4, 8, true>), dim3(4096), dim3(1024), 0, 0, a, b, o, n); });
+    time("flat_w16_def", [&] { hipLaunchKernelGGL((k_flat_w<4, 4, false>), dim3(4096), dim3(1024), 0, 0, a, b, o, n); });
+    time("flat_w16_g1024", [&] { hipLaunchKernelGGL((k_flat_w<4, 4, true>), dim3(1024), dim3(1024), 0, 0, a, b, o, n); });
+    time("flat_w16_g16k", [&] { hipLaunchKernelGGL((k_flat_w<4, 2, true>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
     return 0;
 }
