@@ -12,14 +12,14 @@ reference's own Tsukuba pair (tests/golden/tsukuba.npz), D16 T5.
 RGBA8 in, host maps out, as main.cpp's replacement would call it): ``value``
 stays the device-resident rate (the sum of asw_match's own HIP-event spans,
 h2d end -> consistency end), the PCIe-inclusive wall rate is reported beside it.  N > 1 GPUs (one process per GPU,
-launched by torch.distributed.run) shard the disparity axis of a frame over a
-group of G ranks with RCCL MIN all-reduces for the WTA; G = plan_groups(D, N) is
-the smallest group >= 2 with >= 64 planes per rank (a shard repeats the frame's
-d-independent work, so the fewest shards per frame give the most maps/s: measured
-shard frames in plan_groups' doc), so D=256 runs N/2 concurrent frames, each
-d-sharded over 2 GPUs ("scaling": "weak" past N=2: the per-GPU share stays 1/2
-frame); --group-size 4 / 8 splits one frame wider (lower latency, fewer maps/s).
-`value` counts every frame all groups finished.
+launched by torch.distributed.run) shard the disparity axis of ONE frame over all
+N ranks with RCCL MIN all-reduces for the WTA (BASELINE.json config 4: "d-axis
+sharded across 8x MI355X via RCCL"; at N = 8 each rank owns 32 of the 256 planes
+and runs the half-wave passes of asw_pass32.h): "scaling": "strong", the frame's
+total work is fixed.  ``--group-size G`` splits the N ranks into N/G concurrent
+frames of G shards instead; without it, the layout with the most maps/s,
+plan_groups(D, N) ranks per frame, is timed after the main run and reported beside
+``value`` as ``frame_groups`` (not as ``value``).
 
 Rank 0 prints ONE JSON line.  ``roofline`` is the dominant kernel: the V
 aggregation pass with cached denominators (k_vpass10, DEN_READ: r-1 of the 2r
@@ -82,7 +82,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--group-size", type=int, default=0,
-                    help="ranks per d-sharded frame (0: plan_groups, the smallest group >= 2 with >= 64 planes per rank)")
+                    help="ranks per d-sharded frame (0: one frame over all ranks; the plan_groups layout is timed "
+                         "beside it as frame_groups)")
     return ap.parse_args()
 
 
@@ -235,7 +236,7 @@ def main():
     W, H, D, T, iters, lr, desc = WORKLOADS[args.workload]
     batch = BATCH.get(args.workload, 1)
     lr_mode = 1 if D > 256 else 0  # the 8-bit codes collide above 256 levels: compare indices
-    G = args.group_size or plan_groups(D, world)
+    G = args.group_size or world
     if world % G != 0:
         raise SystemExit(f"--group-size {G} does not divide {world} ranks")
     if args.api == "frame" and world > 1:
@@ -354,6 +355,35 @@ def main():
             torch.cuda.synchronize()
             v_none.append(e[0].elapsed_time(e[1]))
             h_none.append(e[1].elapsed_time(e[2]))
+    # the layout with the most maps/s (plan_groups: N/g concurrent frames of g shards),
+    # timed after the main run and reported beside `value`
+    frame_groups = None
+    g2 = plan_groups(D, world) if world > 1 and not args.group_size and not frame else 1
+    if 1 < g2 < world:
+        subs2 = [dist.new_group(list(range(g * g2, (g + 1) * g2)), backend="gloo" if rehearsal else None)
+                 for g in range(world // g2)]
+        m2 = ShardedStereoMatcher(p, rank % g2, g2, dev, group=subs2[rank // g2])
+        for _ in range(2):
+            for b in range(batch):
+                m2.match(*pairs[b])
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            for b in range(batch):
+                m2.match(*pairs[b])
+        torch.cuda.synchronize()
+        dist.barrier()
+        el2 = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(el2, op=dist.ReduceOp.MAX)
+        n2 = world // g2 * args.steps * batch
+        frame_groups = {"group_size": g2, "frames_per_step": world // g2 * batch,
+                        "value": round(n2 / el2.item(), 4), "unit": "maps/s",
+                        "ms_per_step": round(el2.item() / args.steps * 1000, 4),
+                        "planes_per_rank": m2.p.d_stop - m2.p.d_begin,
+                        "note": f"{world // g2} concurrent frames, each d-sharded over {g2} GPUs "
+                                "(the most maps/s on N GPUs; not the headline layout)"}
+        del m2
     mean = lambda xs: float(np.mean(xs)) if xs else float("nan")  # noqa: E731
     all_pass = v_rd + h_rd + v_wr + h_wr
     stats = torch.tensor([elapsed, mean(v_rd), mean(h_rd), mean(v_wr), mean(h_wr), mean(all_pass),
@@ -419,6 +449,8 @@ def main():
                              "note": "refinement loop + 3x3 median inside each step (main.cpp:540-623); "
                                      "frame_ms_events = raw cost -> median, the span of the reference's "
                                      "published ASW total (main.cpp:707-708, BASELINE.md §1)"}
+        if frame_groups:
+            out["frame_groups"] = frame_groups
         if frame:
             out["pcie_inclusive"] = {"value": round(n_maps / elapsed, 4), "unit": "maps/s",
                                      "note": "wall clock of asw_match incl. host->device upload and device->host "

@@ -16,7 +16,7 @@
  *
  * Device data layout — NOT the reference's plane-major one:
  *   images   : row-major RGBA8, [H][W][4]                         (as lodepng decodes)
- *   cost     : PIXEL-major, [H][W][Dp] float32, Dp = asw_disp_pitch(p)
+ *   cost     : PIXEL-major, [H][W][Dp] float32, Dp = asw_disp_pitch(p) (64k, or 32)
  *              element (y,x,k) holds disparity d = p->d_begin + k (k < d_end-d_begin)
  *   supports : [H][W][Tp] float32, Tp = asw_tap_pitch(p); element (y,x,i) = tap i
  *   LUT      : [(R+1)][766] float32 support-weight table, R = (taps-1)/2
@@ -80,7 +80,9 @@ int asw_last_hip_error(void); /* hipError_t of the last ASW_E_HIP */
 int asw_abi_version(void);
 
 /* layout helpers */
-int asw_disp_pitch(const asw_params *p); /* Dp = round_up(d_end-d_begin, 64)          */
+/* Dp = round_up(d_end-d_begin, 64); a shard (d_begin > 0 or d_end < ndisp) of at most
+ * 32 planes: Dp = 32 (its passes hold two pixels per wave, 32 planes each) */
+int asw_disp_pitch(const asw_params *p);
 int asw_tap_pitch(const asw_params *p);  /* Tp = smallest 4k >= taps with k odd        */
 size_t asw_cost_bytes(const asw_params *p);    /* H*W*Dp*4   */
 size_t asw_support_bytes(const asw_params *p); /* H*W*Tp*4   */
@@ -146,8 +148,9 @@ int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const 
  * the pass computes each weight from `right_rgba` (device RGBA8) and the support LUT
  * (asw_support_lut) as asw_support does, so that array is never written nor read.
  * Bit-identical to asw_aggregate_pass_den with wr = asw_support(H, right).  H only,
- * RGB contexts, tap counts with ring kernels (3, 5, 7, 9, 15, 33, 35, 51; see
- * asw_pass_otf_supported): ASW_E_UNSUPPORTED otherwise. */
+ * RGB contexts, tap counts with ring kernels (3, 5, 7, 9, 15, 33, 35, 51), not a
+ * 32-plane shard (asw_disp_pitch 32; see asw_pass_otf_supported): ASW_E_UNSUPPORTED
+ * otherwise. */
 int asw_aggregate_pass_otf(const asw_params *p, int dir, const float *wl, const uint8_t *right_rgba,
                            const float *lut, const float *cin, float *cout, float *den, int den_mode, void *stream);
 /* 1 when asw_aggregate_pass_otf supports (p, dir), else 0 */
@@ -157,7 +160,8 @@ int asw_pass_otf_supported(const asw_params *p, int dir);
  * K/asw_aggr.cl:3-23) fused: each window element's raw AD/TAD cost is computed
  * from the two RGBA8 images (device pointers) instead of read from a raw-cost
  * volume, so that volume is never written nor read.  cout (and den per den_mode)
- * are bit-identical to asw_raw_cost followed by asw_aggregate_pass_den(V). */
+ * are bit-identical to asw_raw_cost followed by asw_aggregate_pass_den(V).  Ring tap
+ * counts, not a 32-plane shard: ASW_E_UNSUPPORTED otherwise. */
 int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
                            const uint8_t *right_rgba, float *cout, float *den, int den_mode, void *stream);
 
@@ -270,7 +274,8 @@ int asw_refine(const asw_params *p, const asw_refine_params *rp, const uint8_t *
  * variants; returns the previous value, or ASW_E_INVALID for an unknown key.
  * Every variant computes bit-identical results. */
 #define ASW_TUNE_PASS_VARIANT 1
-#define ASW_TUNE_WTA_VARIANT 2 /* 0: lane-per-pixel scan (default), 1: wave-per-pixel reduction */
+#define ASW_TUNE_WTA_VARIANT 2 /* asw_wta: 0 row sweep (default; lane-per-pixel scan where not built),
+                                  1 wave-per-pixel reduction, 2 lane-per-pixel scan */
 int asw_tune_set(int key, int value);
 /* the kernel instantiation the most recent aggregation-pass launch of (dir, den_mode)
  * in this process ran, e.g. "k_vpass10<T=35,NW=16,DM=2,nt>" (NUL-terminated, at most

@@ -16,9 +16,24 @@ int g_pass_variant = 0;
 template <int T, int DM>
 int launch_pass_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                    float *den, hipStream_t st, const RawSrc *raw, const OtfSrc *otf);
+template <int T, int DM>
+int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                     float *den, hipStream_t st);
+// a shard of <= 32 planes (pitch 32): the half-wave passes of asw_pass32.h
+template <int T>
+int launch_pass32_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                    float *den, int dm, hipStream_t st) {
+    if (dm == 1) return launch_pass32_tm<T, 1>(p, dir, wl, wr, cin, cout, den, st);
+    if (dm == 2) return launch_pass32_tm<T, 2>(p, dir, wl, wr, cin, cout, den, st);
+    return launch_pass32_tm<T, 0>(p, dir, wl, wr, cin, cout, den, st);
+}
 template <int T>
 int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                   float *den, int dm, hipStream_t st, const RawSrc *raw, const OtfSrc *otf) {
+    if (asw_disp_pitch(p) == 32) {
+        if (raw || otf) return ASW_E_UNSUPPORTED;  // the fused raw cost and on-the-fly weights: 64-lane passes only
+        return launch_pass32_t<T>(p, dir, wl, wr, cin, cout, den, dm, st);
+    }
     if (dm == 1) return launch_pass_tm<T, 1>(p, dir, wl, wr, cin, cout, den, st, raw, otf);
     if (dm == 2) return launch_pass_tm<T, 2>(p, dir, wl, wr, cin, cout, den, st, raw, otf);
     return launch_pass_tm<T, 0>(p, dir, wl, wr, cin, cout, den, st, raw, otf);

@@ -582,7 +582,13 @@ extern "C" {
 // asw_create rejects shapes the pass kernels cannot address (ASW_E_UNSUPPORTED)
 int asw_abi_version(void) { return ASW_ABI_VERSION; }
 
+// 0: row sweep for asw_WTA (lane-per-pixel scans for the sharded halves), 1: wave per
+// pixel, 2: the lane-per-pixel scan for asw_WTA too (round 3's default)
 static int g_wta_variant = 0;
+namespace asw {
+int launch_wta_sweep(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
+                     float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, hipStream_t st);
+}
 
 int asw_tune_set(int key, int value) {
     if (key == ASW_TUNE_PASS_VARIANT) {
@@ -592,7 +598,7 @@ int asw_tune_set(int key, int value) {
         return asw::set_pass_variant(value);
     }
     if (key == ASW_TUNE_WTA_VARIANT) {
-        if (value != 0 && value != 1) return ASW_E_INVALID;
+        if (value < 0 || value > 2) return ASW_E_INVALID;
         const int old = g_wta_variant;
         g_wta_variant = value;
         return old;
@@ -644,7 +650,13 @@ const char *asw_strerror(int s) {
 
 int asw_last_hip_error(void) { return g_last_hip_error; }
 
-int asw_disp_pitch(const asw_params *p) { return round_up(d_end_of(p) - p->d_begin, 64); }
+int asw_disp_pitch(const asw_params *p) {
+    const int n = d_end_of(p) - p->d_begin;
+    // a d-shard of at most 32 planes (the C4 frame over 8 GPUs): pitch 32, the
+    // half-wave passes of asw_pass32.h; otherwise whole 64-plane blocks
+    if (n <= 32 && (p->d_begin > 0 || d_end_of(p) < p->ndisp)) return 32;
+    return round_up(n, 64);
+}
 int asw_tap_pitch(const asw_params *p) { return tap_pitch(p->taps); }
 size_t asw_cost_bytes(const asw_params *p) {
     return (size_t)p->width * p->height * (size_t)asw_disp_pitch(p) * sizeof(float);
@@ -791,7 +803,9 @@ int asw_aggregate_pass_otf(const asw_params *p, int dir, const float *wl, const 
 
 int asw_pass_otf_supported(const asw_params *p, int dir) {
     if (!p || asw_params_check(p) != ASW_OK) return 0;
-    return dir == ASW_DIR_H && p->color_space == ASW_COLOR_RGB && asw::ring_taps(p->taps) ? 1 : 0;
+    // (a 32-plane shard's half-wave H pass reads the materialised array)
+    return dir == ASW_DIR_H && p->color_space == ASW_COLOR_RGB && asw::ring_taps(p->taps) && asw_disp_pitch(p) != 32
+               ? 1 : 0;
 }
 
 int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
@@ -828,7 +842,12 @@ int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_
     ASW_CHECK_PARAMS(p);
     if (p->d_begin != 0 || d_end_of(p) != p->ndisp) return ASW_E_INVALID;  // sharded: use asw_wta_local & co.
     if (!cost || !d_ref || !conf_ref || !d_tar || !conf_tar) return ASW_E_INVALID;
-    if (g_wta_variant == 0)
+    if (g_wta_variant == 0) {  // the row sweep (asw_wta_sweep.hip) where built for the pitch
+        const int s = asw::launch_wta_sweep(p, cost, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar,
+                                            (hipStream_t)stream);
+        if (s != ASW_E_UNSUPPORTED) return s;
+    }
+    if (g_wta_variant != 1)
         return asw::launch_wta_scan(p, 0, cost, nullptr, nullptr, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar,
                                     (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
@@ -841,7 +860,7 @@ int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_
 int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m1, float *m2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !key || !m1 || !m2) return ASW_E_INVALID;
-    if (g_wta_variant == 0)
+    if (g_wta_variant != 1)
         return asw::launch_wta_local_scan(p, cost, nullptr, reinterpret_cast<long long *>(key), m1, m2,
                                           (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
@@ -856,7 +875,7 @@ int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *
                          float *t2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
-    if (g_wta_variant == 0)
+    if (g_wta_variant != 1)
         return asw::launch_wta_target_local_scan(p, cost, reinterpret_cast<const long long *>(key_ref), nullptr,
                                                  reinterpret_cast<long long *>(tkey), t1, t2, (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
@@ -872,7 +891,7 @@ int asw_wta_ref_local(const asw_params *p, const float *cost, const float *ref_l
                       void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !ref_l || !key || !m1 || !m2) return ASW_E_INVALID;
-    if (g_wta_variant == 0)
+    if (g_wta_variant != 1)
         return asw::launch_wta_local_scan(p, cost, ref_l, reinterpret_cast<long long *>(key), m1, m2,
                                           (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;
@@ -887,7 +906,7 @@ int asw_wta_ref_target_local(const asw_params *p, const float *cost, const float
                              int64_t *tkey, float *t1, float *t2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !ref_r || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
-    if (g_wta_variant == 0)
+    if (g_wta_variant != 1)
         return asw::launch_wta_target_local_scan(p, cost, reinterpret_cast<const long long *>(key_ref), ref_r,
                                                  reinterpret_cast<long long *>(tkey), t1, t2, (hipStream_t)stream);
     const long long n = (long long)p->width * p->height;

@@ -1,0 +1,452 @@
+// asw_pass32.h — the aggregation passes for a disparity shard of at most 32 planes
+// (pitch Dp = 32; asw_disp_pitch).  The C4 frame d-sharded over 8 GPUs gives each
+// GPU 32 of its 256 planes (BASELINE.json config 4); the 64-lane passes
+// of asw_aggregate_impl.h would pad that shard to 64 planes and move twice its cost
+// bytes.  Same tap sequence as every other pass (K/asw_vcost_aggregation.cl:33-40,
+// K/asw_hcost_aggregation.cl:34-41; FP policy in DESIGN.md): bit-identical outputs.
+//
+// A wave holds 32 planes of TWO pixels: lane l is plane p = l & 31 of pixel half
+// h = l >> 5.  The left weight wl_i of a voxel is then per HALF, not per wave, so it
+// cannot be a scalar operand as in the 64-lane passes: the block stages the left
+// support entries it needs in LDS beside the right ones, and each lane reads its
+// half's entry with ds_read_b128 (the 16-lane groups of a b128 read lie inside one
+// half, so a read is a broadcast: as cheap as a right-weight read).
+//   k_vpass32: 16 waves = 32 columns; wave w holds columns x0+w (h=0) and x0+w+16
+//              (h=1), sweeping rows.  One slab per row: the 63 right entries
+//              xr = x0-d0-31 .. x0+31-d0 and the 32 left entries, in an LDS ring
+//              of rows as k_vpass10.
+//   k_hpass32: a wave holds rows y (h=0) and y+1 (h=1) of one row segment, sweeping
+//              x; its right and left entries live in a wave-private LDS ring per row
+//              (no block barrier: the waves of a block share nothing).
+#pragma once
+#include "asw_aggregate_impl.h"
+
+namespace asw {
+namespace agg {
+
+constexpr int kPlanes32 = 32;
+
+// taps [B, E) of a phase with per-lane left weights (wl, wr hold taps from B)
+template <int U, int S, int B, int E, bool DEN, int M>
+__device__ __forceinline__ void taps32(float &num, float &den, const f4 (&wl)[M], const f4 (&wr)[M],
+                                       const float (&win)[U]) {
+#pragma unroll
+    for (int i = B; i < E; ++i) {
+        const float ww = wl[(i - B) / 4][(i - B) % 4] * wr[(i - B) / 4][(i - B) % 4];
+        num = __builtin_fmaf(ww, win[(S + i) % U], num);
+        if constexpr (DEN) den = den + ww;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_vpass32: V pass over a 32-plane shard.  Block = NW waves = 2*NW columns
+// [x0, x0 + 2 NW): wave w holds column x0 + w in lanes 0-31 and x0 + w + NW in
+// lanes 32-63.  Rows are swept as in k_vpass10 (U-row chunks, running offsets, an
+// NBUF-deep LDS ring of row slabs written LEAD rows ahead, one barrier per RB rows,
+// weights in NPH phases with two phases' sets live).
+// ---------------------------------------------------------------------------
+template <int T, int NW, int DM, int CP, int NPH, int RB = 2, int PS = 4>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 4 : 2))) void k_vpass32(
+    const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
+    float *__restrict__ den, int W, int H, int d_begin, int rows_per_strip, int nxb, int nstrip, int xg_per_xcd) {
+    constexpr int R = T / 2;
+    constexpr int TP = tap_pitch(T);
+    constexpr int Q = TP / 4;
+    constexpr int U = pf9_period(T);
+    constexpr int P = U - T;
+    constexpr int KD = 2;  // den prefetch ring (rows)
+    constexpr int LEAD = RB + 1;
+    constexpr int NBUF = ring_div(U, 2 * RB + 1);
+    static_assert(U % PS == 0 && U % KD == 0 && U % RB == 0 && U % NBUF == 0, "ring periods");
+    static_assert(LEAD <= PS, "staging ring too short for the barrier period");
+    constexpr int LA = cmax(cmax(R + P, LEAD + PS), KD);  // rows past y a step touches
+    constexpr int NC = 2 * NW;                             // columns per block
+    constexpr int NER = NC + 31;                           // right entries per row
+    constexpr int NE = NER + NC;                           // + the left entries
+    constexpr int NQ = NE * Q;
+    constexpr int NSTAGE = (NQ + NW * 64 - 1) / (NW * 64);
+    static_assert(NSTAGE <= 2, "slab row larger than two float4 per thread");
+    __shared__ f4 slab[NBUF][NQ];
+
+    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int xg = xcd * xg_per_xcd + m % xg_per_xcd;
+    const int strip = m / xg_per_xcd;
+    if (xg >= nxb || strip >= nstrip) return;  // padding block (uniform)
+    const int x0 = xg * NC;
+    const int y_begin = strip * rows_per_strip;
+    if (y_begin >= H) return;
+    const int y_end = min(H, y_begin + rows_per_strip);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int half = lane >> 5, pl = lane & 31;
+    const int xc = min(x0 + wave + NW * half, W - 1);  // columns past the right edge recompute W-1
+    const int my_wr = ((xc - x0) + 31 - pl) * Q;       // entry xr = xc - d_begin - pl
+    const int my_wl = (NER + (xc - x0)) * Q;
+    const long long rowstride = (long long)W * kPlanes32;
+    const int rowbytes = (int)(rowstride * 4);  // U+LA rows < 2 GiB: checked by the launcher
+    const long long colbase = (long long)x0 * kPlanes32;
+    const int voff = ((xc - x0) * kPlanes32 + pl) * 4;
+    const long long wrow = (long long)W * TP;  // floats per support row
+    auto rsrc_at = [&](const float *base, int row) __attribute__((always_inline)) {
+        return make_rsrc(base + (long long)row * rowstride + colbase);
+    };
+
+    // slab row staging: thread share t0 (t1) = float4 q of entry e; entries < NER are
+    // right weights of xr = x0 - d_begin - 31 + e, the rest left weights of column
+    // x0 + e - NER (both clamped into the row); surplus threads redo the last one
+    const int t0 = min((int)threadIdx.x, NQ - 1);
+    const int t1 = min((int)threadIdx.x + NW * 64, NQ - 1);
+    auto src_of = [&](int t) __attribute__((always_inline)) {
+        const int e = t / Q, q = t - e * Q;
+        if (e < NER) return wr + clampi(x0 - d_begin - 31 + e, 0, W - 1) * TP + 4 * q;
+        return wl + min(x0 + e - NER, W - 1) * TP + 4 * q;
+    };
+    const float *src0 = src_of(t0), *src1 = src_of(t1);
+    auto stage = [&](f4 &a, f4 &b, int row) __attribute__((always_inline)) {
+        a = *reinterpret_cast<const f4 *>(src0 + row * wrow);
+        if constexpr (NSTAGE > 1) b = *reinterpret_cast<const f4 *>(src1 + row * wrow);
+    };
+    auto put = [&](int buf, const f4 &a, const f4 &b) __attribute__((always_inline)) {
+        slab[buf][t0] = a;
+        if constexpr (NSTAGE > 1) slab[buf][t1] = b;
+    };
+
+    using PH = Phases<T, NPH>;
+    float win[U];
+    f4 sa[PS], sb[PS];
+    f4 wlp[NPH][PH::NG], wrp[NPH][PH::NG];
+    float dring[KD];
+    {
+        const int r0 = max(0, y_begin - R);
+        const rsrc_t rp = rsrc_at(cin, r0);
+#pragma unroll
+        for (int j = 0; j < U - 1; ++j) win[j] = bload<CP>(rp, voff, (clampi(y_begin - R + j, 0, H - 1) - r0) * rowbytes);
+    }
+    if constexpr (DM == DM_READ) {
+        const rsrc_t rp = rsrc_at(den, y_begin);
+#pragma unroll
+        for (int j = 0; j < KD; ++j) dring[j] = bload<CP>(rp, voff, (min(y_begin + j, H - 1) - y_begin) * rowbytes);
+    }
+#pragma unroll
+    for (int j = 0; j < PS; ++j) stage(sa[j], sb[j], min(y_begin + j, H - 1));
+#pragma unroll
+    for (int j = 0; j < LEAD; ++j) put(j, sa[j], sb[j]);
+#pragma unroll
+    for (int j = 0; j < LEAD; ++j) stage(sa[j], sb[j], min(y_begin + PS + j, H - 1));
+    __syncthreads();
+    auto request = [&](auto kc, int buf) __attribute__((always_inline)) {
+        constexpr int k = decltype(kc)::value;
+        read_wr<T, PH::gb(k), PH::gb(k + 1)>(wlp[k], &slab[buf][my_wl]);
+        read_wr<T, PH::gb(k), PH::gb(k + 1)>(wrp[k], &slab[buf][my_wr]);
+    };
+    request(std::integral_constant<int, 0>{}, 0);
+
+    auto chunk = [&](auto clamp_c, int ys) __attribute__((always_inline)) {
+        constexpr bool CLAMP = decltype(clamp_c)::value;
+        const int cb = min(ys + R + P, H - 1);
+        const rsrc_t rc = rsrc_at(cin, cb);
+        const rsrc_t ro = rsrc_at(cout, ys);
+        const rsrc_t rd = rsrc_at(den, ys);
+        const rsrc_t rdn = rsrc_at(den, min(ys + KD, H - 1));
+        int so = 0;  // (y - ys) * rowbytes
+        static_for<0, U>([&](auto sc) __attribute__((always_inline)) {
+            constexpr int s = decltype(sc)::value;
+            const int y = ys + s;
+            if constexpr (CLAMP) {
+                if (y >= y_end) return;
+            }
+            constexpr int bcur = s % NBUF, bnext = (s + 1) % NBUF, bput = (s + LEAD) % NBUF;
+            float num = 1e-5f, dn = 1e-5f;
+            static_for<0, NPH>([&](auto kc) __attribute__((always_inline)) {
+                constexpr int k = decltype(kc)::value;
+                // (lgkmcnt 0) phase k's weights are in; at k = 0 every RB rows, also the
+                // slab rows up to y + RB (barrier)
+                if constexpr (k == 0 && s % RB == 0) __syncthreads();
+                else wait_lgkm0();
+                if constexpr (k == 0) asm volatile("" ::"v"(win[(s + T - 1) % U]));  // one vmcnt wait per step
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (k + 1 < NPH) request(std::integral_constant<int, k + 1>{}, bcur);
+                else request(std::integral_constant<int, 0>{}, bnext);
+                if constexpr (k == 0) {
+                    put(bput, sa[(s + LEAD) % PS], sb[(s + LEAD) % PS]);
+                    stage(sa[(s + LEAD) % PS], sb[(s + LEAD) % PS], min(y + LEAD + PS, H - 1));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                taps32<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wlp[k], wrp[k], win);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            if constexpr (DM == DM_READ) {
+                dn = dring[s % KD];
+                dring[s % KD] = bload<CP>(rdn, voff, CLAMP ? (min(y + KD, H - 1) - min(ys + KD, H - 1)) * rowbytes : so);
+            } else if constexpr (DM == DM_WRITE) {
+                bstore<CP>(dn, rd, voff, so);
+            }
+            bstore<CP>(div_pos(num, dn), ro, voff, so);
+            win[(s + U - 1) % U] = bload<CP>(rc, voff, CLAMP ? (min(y + R + P, H - 1) - cb) * rowbytes : so);
+            so += rowbytes;
+            asm volatile("" : "+s"(so));
+        });
+    };
+    int ys = y_begin;
+    for (; ys + U <= y_end && ys + U - 1 + LA <= H - 1; ys += U) chunk(std::false_type{}, ys);
+    for (; ys < y_end; ys += U) {  // the chunks that reach the image bottom, and the partial last chunk
+        asm volatile("" : "+s"(ys));
+        chunk(std::true_type{}, ys);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_hpass32: H pass over a 32-plane shard.  A wave = rows y (lanes 0-31) and y+1
+// (lanes 32-63) of one row segment [xs, xe), sweeping x; block = NWB such waves
+// (independent).  Per row the wave keeps a private LDS ring of right entries
+// (slot = xr mod RING; at step x lane p reads xr = x - d_begin - p) and of left
+// entries (slot = x mod LRING), refilled K entries at a time from one float4 per
+// lane loaded a batch ahead.  The wave reads only what it wrote itself, in program
+// order (LDS operations of a wave complete in order): no barrier.
+//   Batch b (steps [xb, xb+K)) reads right entries [xb-d0-31, xb+K-d0] and left
+//   entries [xb, xb+K] (the last ones: half A... phase 0 of the next step); its top
+//   writes batch b+1's new ones: right [xb+K+1-d0, xb+2K-d0], left [xb+K+1, xb+2K].
+// ---------------------------------------------------------------------------
+constexpr int h32_batch(int T) { return tap_pitch(T) / 4 * 8 <= 64 * 4 ? 4 : 2; }
+
+template <int T, int NWB, int DM, int CP, int NPH>
+__global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(2))) void k_hpass32(
+    const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
+    float *__restrict__ den, int W, int H, int d_begin, int nseg, int seg_len, int npairs, int pairs_per_xcd) {
+    constexpr int R = T / 2;
+    constexpr int TP = tap_pitch(T);
+    constexpr int Q = TP / 4;
+    constexpr int U = pf9_period(T);
+    constexpr int P = U - T;
+    constexpr int KD = 4;  // den prefetch ring (steps)
+    constexpr int K = h32_batch(T);
+    constexpr int RING = (32 + 2 * K + 15) / 16 * 16;  // right entries per row (multiple of 16: conflict-free wrap)
+    constexpr int LRING = 2 * K + 2;                   // left entries per row
+    constexpr int ROWE = RING + LRING;                 // ring entries per row
+    static_assert(U % K == 0, "the batch top must be a compile-time step");
+    // staged per batch: 2 rows x (K right + K left entries) x Q float4 over 64 lanes
+    constexpr int NST = 4 * K * Q;
+    constexpr int SPL = (NST + 63) / 64;  // float4 per lane
+    __shared__ f4 ring_all[NWB][2 * ROWE * Q];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // work item = (row pair, segment); XCD-aware: consecutive items on one XCD
+    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int item_l = m * NWB + wave;
+    if (item_l >= pairs_per_xcd) return;  // whole wave
+    const int item = xcd * pairs_per_xcd + item_l;
+    if (item >= npairs) return;
+    const int pr = item / nseg;
+    const int xs = (item - pr * nseg) * seg_len;
+    const int xe = min(xs + seg_len, W);
+    const int half = lane >> 5, pl = lane & 31;
+    const int y = min(2 * pr + half, H - 1);  // an odd last row: both halves on it (same values, same place)
+    const int d0 = d_begin;
+    f4 *ring = ring_all[wave];
+    f4 *myrow = ring + half * ROWE * Q;
+
+    // staging share j of lane l: float4 n = j*64 + l of the batch's NST, with
+    // n = ((r*2 + kind)*K + k)*Q + q: row r, kind 0 = right entry xb+1-d0+k, kind 1 =
+    // left entry xb+1+k of the batch whose first step is xb (its entries are written at
+    // the top of batch xb - K, the batch before the one that first reads them)
+    const float *wrrows[2] = {wr + (long long)min(2 * pr, H - 1) * W * TP, wr + (long long)min(2 * pr + 1, H - 1) * W * TP};
+    const float *wlrows[2] = {wl + (long long)min(2 * pr, H - 1) * W * TP, wl + (long long)min(2 * pr + 1, H - 1) * W * TP};
+    const float *st_row[SPL];
+    int st_q4[SPL], st_k[SPL], st_kind[SPL], st_slot[SPL], st_base[SPL];
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+        const int n = min(j * 64 + lane, NST - 1);
+        const int q = n % Q, k = (n / Q) % K, kind = (n / (Q * K)) & 1, r = n / (2 * Q * K);
+        st_row[j] = kind == 0 ? wrrows[r] : wlrows[r];
+        st_q4[j] = 4 * q;
+        st_k[j] = k;
+        st_kind[j] = kind;
+        // LDS float4 index of the entry for the first top (xb = xs: entries of batch xs + K)
+        const int e = xs + K + 1 + k;
+        st_slot[j] = kind == 0 ? (r * ROWE + (e - d0 + (1 << 20)) % RING) * Q + q
+                               : (r * ROWE + RING + e % LRING) * Q + q;
+        st_base[j] = kind == 0 ? r * ROWE * Q : (r * ROWE + RING) * Q;
+    }
+    auto st_load = [&](int j, int xb) __attribute__((always_inline)) {  // entry of the batch starting at xb
+        const int e = xb + 1 + st_k[j];
+        const int c = st_kind[j] == 0 ? clampi(e - d0, 0, W - 1) : min(e, W - 1);
+        return *reinterpret_cast<const f4 *>(st_row[j] + c * TP + st_q4[j]);
+    };
+
+    // the rings before step xs: right entries [xs-d0-31, xs+K-d0], left [xs, xs+K]
+    constexpr int NR0 = 32 + K, NL0 = K + 1;
+    for (int t = lane; t < 2 * (NR0 + NL0) * Q; t += 64) {
+        const int q = t % Q, ee = t / Q;
+        const int r = ee / (NR0 + NL0), e = ee % (NR0 + NL0);
+        f4 v;
+        int slot;
+        if (e < NR0) {
+            const int xr = xs - d0 - 31 + e;
+            v = *reinterpret_cast<const f4 *>(wrrows[r] + clampi(xr, 0, W - 1) * TP + 4 * q);
+            slot = (xr + (1 << 20)) % RING;
+        } else {
+            const int x = xs + e - NR0;
+            v = *reinterpret_cast<const f4 *>(wlrows[r] + min(x, W - 1) * TP + 4 * q);
+            slot = RING + x % LRING;
+        }
+        ring[(r * ROWE + slot) * Q + q] = v;
+    }
+    f4 stg[SPL];
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) stg[j] = st_load(j, xs + K);
+
+    const long long rowoff = (long long)y * W * kPlanes32;
+    const rsrc_t rc = make_rsrc(cin + rowoff);
+    const rsrc_t ro = make_rsrc(cout + rowoff);
+    const rsrc_t rd = make_rsrc(den + rowoff);
+    const int voff = pl * 4;
+    constexpr int xstride = kPlanes32 * 4;  // bytes per column
+    // LDS float4 index of this lane's entries at step x
+    auto wr_at = [&](int x) __attribute__((always_inline)) {
+        return myrow + ((x - d0 - pl + (1 << 20)) % RING) * Q;
+    };
+    auto wl_at = [&](int x) __attribute__((always_inline)) { return myrow + (RING + x % LRING) * Q; };
+
+    using PH = Phases<T, NPH>;
+    float win[U];
+    f4 wlp[NPH][PH::NG], wrp[NPH][PH::NG];
+    float dring[KD];
+#pragma unroll
+    for (int j = 0; j < U - 1; ++j) win[j] = bload<CP>(rc, voff, clampi(xs - R + j, 0, W - 1) * xstride);
+    if constexpr (DM == DM_READ) {
+#pragma unroll
+        for (int j = 0; j < KD; ++j) dring[j] = bload<CP>(rd, voff, min(xs + j, W - 1) * xstride);
+    }
+    auto request = [&](auto kc, int x) __attribute__((always_inline)) {
+        constexpr int k = decltype(kc)::value;
+        read_wr<T, PH::gb(k), PH::gb(k + 1)>(wlp[k], wl_at(x));
+        read_wr<T, PH::gb(k), PH::gb(k + 1)>(wrp[k], wr_at(x));
+    };
+    request(std::integral_constant<int, 0>{}, xs);
+
+    auto body = [&](auto sc, auto chk, int xb) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc)::value;
+        constexpr bool CHK = decltype(chk)::value;
+        const int x = xb + s;
+        if constexpr (CHK) {
+            if (x >= xe) return;
+        }
+        if constexpr (s % K == 0) {
+            // top of a batch (steps [x, x+K)): write the entries the next batch reads
+            // first (loaded a batch ago), then load the ones after them
+#pragma unroll
+            for (int j = 0; j < SPL; ++j) {
+                ring[st_slot[j]] = stg[j];
+                // advance the slot by K entries inside its ring (RING or LRING entries)
+                const int lim = st_kind[j] == 0 ? RING * Q : LRING * Q;
+                int rel = st_slot[j] - st_base[j] + K * Q;
+                rel = rel >= lim ? rel - lim : rel;
+                st_slot[j] = st_base[j] + rel;
+            }
+#pragma unroll
+            for (int j = 0; j < SPL; ++j) stg[j] = st_load(j, x + 2 * K);
+        }
+        float num = 1e-5f, dn = 1e-5f;
+        static_for<0, NPH>([&](auto kc) __attribute__((always_inline)) {
+            constexpr int k = decltype(kc)::value;
+            wait_lgkm0();
+            if constexpr (k == 0) asm volatile("" ::"v"(win[(s + T - 1) % U]));  // one vmcnt wait per step
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (k + 1 < NPH) request(std::integral_constant<int, k + 1>{}, x);
+            else request(std::integral_constant<int, 0>{}, x + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            taps32<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wlp[k], wrp[k], win);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        const int xo = x * xstride;
+        if constexpr (DM == DM_READ) {
+            dn = dring[s % KD];
+            dring[s % KD] = bload<CP>(rd, voff, min(x + KD, W - 1) * xstride);
+        } else if constexpr (DM == DM_WRITE) {
+            bstore<CP>(dn, rd, voff, xo);
+        }
+        bstore<CP>(div_pos(num, dn), ro, voff, xo);
+        win[(s + U - 1) % U] = bload<CP>(rc, voff, min(x + R + P, W - 1) * xstride);
+    };
+    int xb = xs;
+    for (; xb + U <= xe; xb += U)
+        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::false_type{}, xb); });
+    if (xb < xe) static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::true_type{}, xb); });
+}
+
+// ---------------------------------------------------------------------------
+// launchers (one (T, DM) per translation unit: build/p32_t<T>_d<DM>.hip)
+// ---------------------------------------------------------------------------
+template <int T, int NW, int DM, int CP, int NPH>
+void launch_v32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
+                hipStream_t st) {
+    constexpr int U = pf9_period(T);
+    const int W = p->width, H = p->height;
+    const int nxb = (W + 2 * NW - 1) / (2 * NW);
+    // row strips: enough blocks for the 256 CUs (NW = 16: one block per CU), strips of
+    // whole U-row chunks, >= 2T rows (the window prologue, U-1 row loads per strip)
+    int nstrip = (int)((512LL * 16 / NW + nxb - 1) / nxb);
+    const int max_strip = H / (2 * T) > 1 ? H / (2 * T) : 1;
+    if (nstrip > max_strip) nstrip = max_strip;
+    if (nstrip < 1) nstrip = 1;
+    const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
+    nstrip = (H + rows - 1) / rows;
+    const int per_xcd = (nxb + 7) / 8;
+    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl, wr, cin,
+                       cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd);
+    note_pass_kernel(ASW_DIR_V, DM, "k_vpass32", T, NW == 16 ? (NPH == 4 ? "NW=16,NPH=4" : "NW=16") : "NW=8,NPH=3",
+                     CP == kCPStream);
+}
+
+template <int T, int NWB, int DM, int CP, int NPH>
+void launch_h32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
+                hipStream_t st, int seg_len) {
+    const int W = p->width, H = p->height;
+    const int nseg = (W + seg_len - 1) / seg_len;
+    const int npairs = (H + 1) / 2 * nseg;  // work items: (row pair, segment)
+    const int per_xcd = (npairs + 7) / 8;
+    const int blocks_per_xcd = (per_xcd + NWB - 1) / NWB;
+    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH>), dim3(8 * blocks_per_xcd), dim3(NWB * 64), 0, st, wl, wr, cin,
+                       cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd);
+    note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T, NWB == 4 ? "NWB=4" : "NWB=2", CP == kCPStream);
+}
+
+template <int T, int DM>
+int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
+                     float *den, hipStream_t st) {
+    constexpr int U = pf9_period(T);
+    const bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
+    if (dir == ASW_DIR_V) {
+        // 16 waves (1024 threads, 4 waves per SIMD: <= 128 VGPRs): the per-lane left
+        // weights take as many registers as the right ones, so T >= 33 keeps two of
+        // four phases' weights live (three phases: 179 VGPRs spilled at T = 35; four:
+        // 118 VGPRs).  T > 35: 8 waves (16 columns), up to 256 VGPRs.
+        constexpr int NW = T > 35 ? 8 : 16;
+        constexpr int NPH = T > 35 ? 3 : T >= 33 ? 4 : 2;
+        if (stream) launch_v32<T, NW, DM, kCPStream, NPH>(p, wl, wr, cin, cout, den, st);
+        else launch_v32<T, NW, DM, 0, NPH>(p, wl, wr, cin, cout, den, st);
+    } else {
+        // segments: the multiple of U nearest W/4 (>= 2 U): at C4 four 480-column
+        // segments per row pair, 2160 waves; the window prologue (U-1 columns) is paid
+        // once per segment
+        int seg = (p->width / 4 + U / 2) / U * U;
+        if (seg < 2 * U) seg = 2 * U;
+        constexpr int NWB = T > 35 ? 2 : 4;
+        if (stream) launch_h32<T, NWB, DM, kCPStream, 2>(p, wl, wr, cin, cout, den, st, seg);
+        else launch_h32<T, NWB, DM, 0, 2>(p, wl, wr, cin, cout, den, st, seg);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_hip_error(e);
+        return ASW_E_HIP;
+    }
+    return ASW_OK;
+}
+
+}  // namespace agg
+}  // namespace asw
+
+#define ASW_INSTANTIATE_PASS32(TT, DM)                                                                            \
+    template int asw::agg::launch_pass32_tm<TT, DM>(const asw_params *, int, const float *, const float *,       \
+                                                    const float *, float *, float *, hipStream_t);

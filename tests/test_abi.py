@@ -68,7 +68,12 @@ def test_layout_pitches(L, D, T, Dp, Tp):
 def test_shard_pitch(L):
     p = L.default_params(10, 10, ndisp=256, taps=35, d_begin=64, d_end=128)
     assert L.disp_pitch(p) == 64
+    # a shard of <= 32 planes: pitch 32 (the half-wave passes, asw_pass32.h)
     p = L.default_params(10, 10, ndisp=256, taps=35, d_begin=0, d_end=32)
+    assert L.disp_pitch(p) == 32
+    p = L.default_params(10, 10, ndisp=256, taps=35, d_begin=250, d_end=256)
+    assert L.disp_pitch(p) == 32
+    p = L.default_params(10, 10, ndisp=32, taps=35)  # the whole range: 64-plane blocks
     assert L.disp_pitch(p) == 64
 
 

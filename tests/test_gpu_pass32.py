@@ -1,0 +1,123 @@
+"""The 32-plane shard passes (k_vpass32 / k_hpass32, asw_pass32.h) — run on an MI355X.
+
+A d-shard of at most 32 planes (the C4 frame split over 8 GPUs: 32 of 256 planes per
+GPU) has pitch Dp = 32 and runs passes that hold two pixels per wave.  Every pass is
+compared bit for bit with the oracle's pass (the reference's tap sequence,
+K/asw_vcost_aggregation.cl:33-40, K/asw_hcost_aggregation.cl:34-41) over the shard's
+planes, in all three denominator modes, on shapes that hit the image edges (W < 32,
+odd heights, a row pair cut by the bottom), for every ring tap count.
+"""
+import numpy as np
+import pytest
+
+from conftest import pixel_major, plane_major
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _params(W, H, D, T, iters=7, **kw):
+    from stereo_matchin_amd import make_params
+    return make_params(W, H, ndisp=D, taps=T, iters=iters, **kw)
+
+
+def _rand_pair(seed, H, W, shift=4):
+    rng = np.random.default_rng(seed)
+    L = rng.integers(0, 256, (H, W, 4), dtype=np.uint8)
+    R = np.roll(L, -shift, axis=1).copy()
+    R[..., :3] = np.clip(R[..., :3].astype(int) + rng.integers(-5, 6, (H, W, 3)), 0, 255).astype(np.uint8)
+    L[..., 3] = 255
+    R[..., 3] = 255
+    return np.ascontiguousarray(L), np.ascontiguousarray(R)
+
+
+def test_pitch_of_small_shards():
+    import stereo_matchin_amd.kernels as K
+    assert K.cost_shape(_params(40, 20, 256, 35, d_begin=224, d_end=256))[2] == 32
+    assert K.cost_shape(_params(40, 20, 256, 35, d_begin=0, d_end=32))[2] == 32
+    assert K.cost_shape(_params(40, 20, 100, 35, d_begin=40, d_end=57))[2] == 32
+    assert K.cost_shape(_params(40, 20, 256, 35, d_begin=0, d_end=33))[2] == 64
+    assert K.cost_shape(_params(40, 20, 16, 5))[2] == 64  # a whole (unsharded) range keeps 64
+
+
+# every ring tap count (other odd T run k_pass_any, pitch 32 too), both directions,
+# a DEN_NONE, a DEN_WRITE and a DEN_READ pass each bit-exact against the oracle
+@pytest.mark.parametrize("T", [3, 5, 7, 9, 11, 15, 33, 35, 51])
+@pytest.mark.parametrize("direction", [0, 1])
+@pytest.mark.parametrize("H,W,D,d0,d1", [(37, 91, 70, 38, 70), (23, 150, 200, 70, 87), (8, 20, 64, 0, 32),
+                                          (9, 331, 256, 224, 256)])
+def test_pass32_bit_exact(gpu, oracle, T, direction, H, W, D, d0, d1):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    Lh, Rh = _rand_pair(T * 5 + direction + W, H, W, shift=6)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
+    Dp = K.cost_shape(p)[2]
+    assert Dp == 32
+    rng = np.random.default_rng(T + D + H)
+    sl, sr = oracle.support(Lh, T, direction), oracle.support(Rh, T, direction)
+    f = K.asw_vSupport if direction == 0 else K.asw_hSupport
+    g = K.asw_vCostAggregation if direction == 0 else K.asw_hCostAggregation
+    wl, wr = f(p, _t(Lh, gpu)), f(p, _t(Rh, gpu))
+    den = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+    for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
+        cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+        want = oracle.aggregate_pass(sl, sr, cin, T, direction, d0=d0, d1=d1, plane_base=d0)
+        out = g(p, wl, wr, _t(pixel_major(cin, Dp), gpu), den=den, den_mode=mode)
+        got = plane_major(_np(out), d1 - d0)
+        assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
+        name = K.pass_kernel(direction, mode)
+        if T in (3, 5, 7, 9, 15, 33, 35, 51):
+            assert name.startswith(("k_vpass32<" if direction == 0 else "k_hpass32<") + f"T={T},"), name
+        else:
+            assert name.startswith("k_pass_any<"), name
+
+
+def test_pass32_rejects_fused_raw_and_otf(gpu):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    p = _params(64, 16, 256, 35, d_begin=224, d_end=256)
+    assert not K.otf_supported(p)
+    x = torch.zeros(K.cost_shape(p), dtype=torch.float32, device=gpu)
+    w = torch.zeros(K.support_shape(p), dtype=torch.float32, device=gpu)
+    img = torch.zeros((16, 64, 4), dtype=torch.uint8, device=gpu)
+    with pytest.raises(_lib.AswError) as e:
+        K.asw_vCostAggregation_raw(p, w, w, img, img, out=x)
+    assert e.value.status == _lib.ASW_E_UNSUPPORTED
+
+
+# the C4 shard of the 8-way split: one rank's 32 planes of a 1920-column D256 T35
+# frame through the whole r = 7 pass sequence, on a full-width band of 215 rows (the
+# oracle's passes over all 1080 rows take minutes), against the oracle on that band
+def test_c4_shard_band_r7(gpu, oracle):
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd.pipeline import StereoMatcher
+    from stereo_matchin_amd.synthetic import make_pair
+    W, H, D, T, r = 1920, 1080, 256, 35, 7
+    Lh, Rh, _ = make_pair(W, H, D, 0)
+    band = 96 + r * (T // 2)
+    d0, d1 = 96, 128  # rank 3 of 8
+    Lb, Rb = np.ascontiguousarray(Lh[:band]), np.ascontiguousarray(Rh[:band])
+    p = _params(W, band, D, T, iters=r, d_begin=d0, d_end=d1)
+    m = StereoMatcher(p, gpu)
+    m.raw_and_support(_t(Lb, gpu), _t(Rb, gpu))
+    got = plane_major(_np(m.aggregate()), d1 - d0)
+    assert K.pass_kernel(0, 2).startswith("k_vpass32<T=35") and K.pass_kernel(1, 2).startswith("k_hpass32<T=35")
+    cost = oracle.raw_cost(Lb, Rb, D)[d0:d1]
+    sv = (oracle.support(Lb, T, 0), oracle.support(Rb, T, 0))
+    sh = (oracle.support(Lb, T, 1), oracle.support(Rb, T, 1))
+    for _ in range(r):
+        cost = oracle.aggregate_pass(*sv, cost, T, 0, d0=d0, d1=d1, plane_base=d0)
+        cost = oracle.aggregate_pass(*sh, cost, T, 1, d0=d0, d1=d1, plane_base=d0)
+    assert np.array_equal(got, cost), np.argwhere(got != cost)[:5]

@@ -128,11 +128,14 @@ def test_frame_api_refine(gpu, oracle):
     assert out["timings"]["refine"] > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1])
-@pytest.mark.parametrize("H,W,D", [(1, 1, 1), (5, 67, 61), (13, 129, 256), (3, 200, 300), (7, 64, 33)])
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("H,W,D", [(1, 1, 1), (5, 67, 61), (13, 129, 256), (3, 200, 300), (7, 64, 33),
+                                   (2, 700, 128), (4, 1000, 256), (3, 63, 200), (2, 300, 2)])
 def test_wta_variants_on_random_volume(gpu, oracle, variant, H, W, D):
-    """asw_WTA: the lane-per-pixel scan (variant 0) and the wave-per-pixel reduction
-    (variant 1) against the oracle on volumes with many exact ties."""
+    """asw_WTA: the row sweep (variant 0, Dp 64 / 128 / 256; the scan elsewhere), the
+    wave-per-pixel reduction (1) and the lane-per-pixel scan (2) against the oracle on
+    volumes with many exact ties (rows longer than the 255-plane diagonals, the clamped
+    first points of pixels x < md, rows not a multiple of 64 pixels)."""
     import stereo_matchin_amd.kernels as K
     from stereo_matchin_amd import _lib
     rng = np.random.default_rng(H * W + D)
@@ -144,5 +147,5 @@ def test_wta_variants_on_random_volume(gpu, oracle, variant, H, W, D):
         got = K.asw_WTA(p, _t(pixel_major(cost, K.cost_shape(p)[2]), gpu))
     finally:
         _lib.lib().asw_tune_set(2, old)
-    for g, w in zip(got[:4], want[:4]):
-        assert np.array_equal(_np(g), w)
+    for i, (g, w) in enumerate(zip(got[:4], want[:4])):
+        assert np.array_equal(_np(g), w), (i, np.argwhere(_np(g) != w)[:5])

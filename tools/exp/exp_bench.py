@@ -102,7 +102,9 @@ def main():
                 "v12_read": (12, 2, 0), "v12_read_s1": (12, 2, 1), "v12_read_s3": (12, 2, 3),
                 "v12_none": (12, 0, 0), "v12_write": (12, 1, 0),
                 "vpx0": ("px0", 2, 0), "vpx4": ("px4", 2, 0), "vpx8": ("px8", 2, 0),
-                "vpx_e": ("px_e", 2, 0), "vpx_f": ("px_f", 2, 0), "vpx_g": ("px_g", 2, 0)}
+                "vpx_e": ("px_e", 2, 0), "vpx_f": ("px_f", 2, 0), "vpx_g": ("px_g", 2, 0),
+                # round 4: 8-column blocks at 4 waves per SIMD (two blocks per CU)
+                "vpx_n8w4": ("px_n8w4", 2, 0)}
         vexps = [(n,) + allv[n] for n in args.vexps.split(",")]
         for rep in range(args.reps + 1):
             for name, kind, dm, ns in vexps:

@@ -54,7 +54,7 @@ for step in "$@"; do
     case "$name" in
         test)
             if [ -n "$arg" ]; then
-                run 900 "pytest_$TAG" $PY -m pytest tests -m gpu -x -v -k "$arg" --timeout 240 --timeout-method thread
+                run 900 "pytest_$TAG" $PY -m pytest tests -m gpu -x -v -k "$args" --timeout 240 --timeout-method thread
             else
                 run 1100 "pytest_$TAG" $PY -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread
             fi ;;

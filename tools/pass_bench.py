@@ -35,12 +35,16 @@ def main():
     ap.add_argument("--variants", default="0")
     ap.add_argument("--den", action="store_true", help="also time the cached-denominator modes (write, read)")
     ap.add_argument("--ndisp", type=int, default=0, help="override D (e.g. a d-shard's local planes)")
+    ap.add_argument("--planes", type=int, default=0,
+                    help="time the shard [0, planes) of the D planes (<= 32: pitch 32, the asw_pass32.h passes)")
     args = ap.parse_args()
     W, H, D, T, iters, lr, desc = WORKLOADS[args.workload]
     D = args.ndisp or D
     dev = torch.device("cuda:0")
     Lh, Rh, _ = make_pair(W, H, D, 0)
     p = make_params(W, H, ndisp=D, taps=T, iters=iters)
+    if args.planes:
+        p.d_begin, p.d_end = 0, args.planes
     m = StereoMatcher(p, dev, otf=False)  # materialised whr too: both H forms are timed
     m.raw_and_support(torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev))
     torch.cuda.synchronize()
@@ -51,9 +55,11 @@ def main():
     dens = {"v": torch.empty_like(cin), "h": torch.empty_like(cin), "h_otf": torch.empty_like(cin)} if args.den else {}
     lib = _lib.lib()
     S = W * H
-    nbytes = 8 * D * S + 8 * T * S
+    nloc = p.d_stop - p.d_begin
+    nbytes = 8 * nloc * S + 8 * T * S
+    dirs = ("v", "h", "h_otf") if K.otf_supported(p) else ("v", "h")
     ref = {}
-    times = {(v, d, dm): [] for v in variants for d in ("v", "h", "h_otf") for dm in modes}
+    times = {(v, d, dm): [] for v in variants for d in dirs for dm in modes}
     for rep in range(args.reps + 1):
         for v in variants:
             lib.asw_tune_set(1, v)
@@ -62,7 +68,7 @@ def main():
                 p_, wl_, right, m.lut, cin_, out=out, den=den, den_mode=den_mode)
             for d, fn, wl, wr in (("v", K.asw_vCostAggregation, m.wvl, m.wvr),
                                   ("h", K.asw_hCostAggregation, m.whl, m.whr),
-                                  ("h_otf", otf, m.whl, None)):
+                                  ("h_otf", otf, m.whl, None))[:len(dirs)]:
                 for dm in modes:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
@@ -81,7 +87,8 @@ def main():
     lib.asw_tune_set(1, 0)
     for (v, d, dm), ts in times.items():
         med = float(np.median(ts))
-        print(json.dumps({"workload": args.workload, "ndisp": D, "variant": v, "dir": d, "den_mode": dm,
+        print(json.dumps({"workload": args.workload, "ndisp": D, "planes": nloc, "variant": v, "dir": d, "den_mode": dm,
+                          "kernel": K.pass_kernel(0 if d == "v" else 1, dm),
                           "ms_median": round(med, 4), "ms_min": round(min(ts), 4),
                           "GBps": round(nbytes / med / 1e6, 1),
                           "frac_of_8TBps": round(nbytes / med / 1e6 / 8000, 4)}))
