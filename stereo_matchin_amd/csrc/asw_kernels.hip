@@ -576,6 +576,12 @@ using namespace asw;
 // ===========================================================================
 // C-ABI: parameters and layout
 // ===========================================================================
+namespace asw {
+// asw_wta_sweep.hip: asw_WTA as a row sweep (ASW_E_UNSUPPORTED for pitches it is not built for)
+int launch_wta_sweep(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
+                     float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, hipStream_t st);
+}  // namespace asw
+
 extern "C" {
 
 // 2: asw_outputs gained disp16 / lr16 and asw_timings gained exchange (round 2);
@@ -585,10 +591,6 @@ int asw_abi_version(void) { return ASW_ABI_VERSION; }
 // 0: row sweep for asw_WTA (lane-per-pixel scans for the sharded halves), 1: wave per
 // pixel, 2: the lane-per-pixel scan for asw_WTA too (round 3's default)
 static int g_wta_variant = 0;
-namespace asw {
-int launch_wta_sweep(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
-                     float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, hipStream_t st);
-}
 
 int asw_tune_set(int key, int value) {
     if (key == ASW_TUNE_PASS_VARIANT) {
