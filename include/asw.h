@@ -274,8 +274,8 @@ int asw_refine(const asw_params *p, const asw_refine_params *rp, const uint8_t *
  * variants; returns the previous value, or ASW_E_INVALID for an unknown key.
  * Every variant computes bit-identical results. */
 #define ASW_TUNE_PASS_VARIANT 1
-#define ASW_TUNE_WTA_VARIANT 2 /* asw_wta: 0 row sweep (default; lane-per-pixel scan where not built),
-                                  1 wave-per-pixel reduction, 2 lane-per-pixel scan */
+#define ASW_TUNE_WTA_VARIANT 2 /* asw_wta: 0 lane-per-pixel scan (default), 1 wave-per-pixel reduction,
+                                  2 row sweep (Dp 64/128/256; the scan elsewhere) */
 int asw_tune_set(int key, int value);
 /* the kernel instantiation the most recent aggregation-pass launch of (dir, den_mode)
  * in this process ran, e.g. "k_vpass10<T=35,NW=16,DM=2,nt>" (NUL-terminated, at most

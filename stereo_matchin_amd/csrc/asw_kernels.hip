@@ -588,8 +588,8 @@ extern "C" {
 // asw_create rejects shapes the pass kernels cannot address (ASW_E_UNSUPPORTED)
 int asw_abi_version(void) { return ASW_ABI_VERSION; }
 
-// 0: row sweep for asw_WTA (lane-per-pixel scans for the sharded halves), 1: wave per
-// pixel, 2: the lane-per-pixel scan for asw_WTA too (round 3's default)
+// 0: lane-per-pixel scans (default), 1: wave per pixel, 2: asw_WTA by the row sweep
+// (asw_wta_sweep.hip; the sharded halves keep the lane-per-pixel scans)
 static int g_wta_variant = 0;
 
 int asw_tune_set(int key, int value) {
@@ -844,7 +844,8 @@ int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_
     ASW_CHECK_PARAMS(p);
     if (p->d_begin != 0 || d_end_of(p) != p->ndisp) return ASW_E_INVALID;  // sharded: use asw_wta_local & co.
     if (!cost || !d_ref || !conf_ref || !d_tar || !conf_tar) return ASW_E_INVALID;
-    if (g_wta_variant == 0) {  // the row sweep (asw_wta_sweep.hip) where built for the pitch
+    if (g_wta_variant == 2) {  // the row sweep (asw_wta_sweep.hip) where built for the pitch: opt-in,
+        // measured 2.21 ms against the scan's 0.57 at C4 (one wave per row: latency-bound)
         const int s = asw::launch_wta_sweep(p, cost, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar,
                                             (hipStream_t)stream);
         if (s != ASW_E_UNSUPPORTED) return s;

@@ -296,11 +296,13 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(2))) v
 #pragma unroll
     for (int j = 0; j < SPL; ++j) stg[j] = st_load(j, xs + K);
 
-    const long long rowoff = (long long)y * W * kPlanes32;
+    // buffer resources at the pair's first row (wave-uniform); half 1 reaches its row
+    // through the lane offset (W * 128 B per row)
+    const long long rowoff = (long long)(2 * pr) * W * kPlanes32;
     const rsrc_t rc = make_rsrc(cin + rowoff);
     const rsrc_t ro = make_rsrc(cout + rowoff);
     const rsrc_t rd = make_rsrc(den + rowoff);
-    const int voff = pl * 4;
+    const int voff = pl * 4 + (y - 2 * pr) * W * kPlanes32 * 4;
     constexpr int xstride = kPlanes32 * 4;  // bytes per column
     // LDS float4 index of this lane's entries at step x
     auto wr_at = [&](int x) __attribute__((always_inline)) {

@@ -32,20 +32,15 @@ from .pipeline import MatchResult, StereoMatcher
 
 
 def plan_groups(ndisp: int, world: int, min_planes: int = 64) -> int:
-    """Ranks per d-sharded frame ("group size") for `world` ranks: the SMALLEST
-    divisor g >= 2 of `world` with ndisp/g >= min_planes (1 if none); world/g groups
-    then each match their own frame, concurrently.
+    """Ranks per d-sharded frame ("group size") for the most maps/s on `world` ranks:
+    the SMALLEST divisor g >= 2 of `world` with ndisp/g >= min_planes (1 if none);
+    world/g groups then each match their own frame, concurrently.
 
-    Why the smallest: a shard repeats the frame's d-independent work (supports, the
-    image staging of the raw cost, the WTA exchange and LR check), and the pass
-    kernels work on 64-plane blocks, so a shard narrower than 64 planes pads up to 64.
-    Measured one-GPU shard frames of C4 (tools/shard_frame_bench.py, no collective,
-    profiles/r03/shard_frames_r08f.log): 128 planes 12.99 ms, 64 planes 7.63 ms,
-    32 planes 7.59 ms, against 23.3 ms for the whole frame.  With ~0.4 ms of RCCL
-    per frame, 8 GPUs give ~298 maps/s as four 2-way groups, ~250 as two 4-way
-    groups and ~125 as one 8-way frame.  So D=256 runs 2-way groups on 2, 4 and 8
-    GPUs; wider splits (lower latency per frame, fewer maps/s) are bench.py
-    --group-size 4 / 8.
+    Why the smallest: a shard repeats the frame's d-independent work (supports and
+    their per-pass reads, the image staging of the raw cost, the WTA exchange and LR
+    check), so the fewest shards per frame give the most frames per GPU-second.
+    bench.py's headline layout is NOT this one: it shards ONE frame over all ranks
+    (BASELINE.json config 4), and reports this layout beside it as ``frame_groups``.
     """
     for g in range(2, world + 1):
         if world % g == 0 and ndisp / g >= min_planes:

@@ -132,8 +132,8 @@ def test_frame_api_refine(gpu, oracle):
 @pytest.mark.parametrize("H,W,D", [(1, 1, 1), (5, 67, 61), (13, 129, 256), (3, 200, 300), (7, 64, 33),
                                    (2, 700, 128), (4, 1000, 256), (3, 63, 200), (2, 300, 2)])
 def test_wta_variants_on_random_volume(gpu, oracle, variant, H, W, D):
-    """asw_WTA: the row sweep (variant 0, Dp 64 / 128 / 256; the scan elsewhere), the
-    wave-per-pixel reduction (1) and the lane-per-pixel scan (2) against the oracle on
+    """asw_WTA: the lane-per-pixel scan (variant 0), the wave-per-pixel reduction (1) and
+    the row sweep (2: Dp 64 / 128 / 256, the scan elsewhere) against the oracle on
     volumes with many exact ties (rows longer than the 255-plane diagonals, the clamped
     first points of pixels x < md, rows not a multiple of 64 pixels)."""
     import stereo_matchin_amd.kernels as K

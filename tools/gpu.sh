@@ -83,7 +83,7 @@ for step in "$@"; do
                 run 300 "traffic_$c" rocprofv3 --pmc $c --output-format csv -d "$OUT/traffic/p$i" -o run -- \
                     python3 bench.py --steps 2 --warmup 1 --no-cpu $args
             done ;;
-        cmd) run 300 "cmd_$TAG" bash -c "$arg" ;;
+        cmd) ncmd=$((${ncmd:-0} + 1)); run 300 "cmd${ncmd}_$TAG" bash -c "$arg" ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
