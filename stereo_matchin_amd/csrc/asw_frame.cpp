@@ -269,7 +269,9 @@ int alloc_shard(Shard &s, bool sharded) {
     ASWCHK(dev_alloc(&s.c0, asw_cost_bytes(p)));
     ASWCHK(dev_alloc(&s.c1, asw_cost_bytes(p)));
     if (p->iters >= 2) {  // the den of a direction is written by its first pass and read by the r-1 others
-        ASWCHK(dev_alloc(&s.den_v, asw_cost_bytes(p)));
+        // (a 32-plane shard's V pass recomputes it: k_vpass32 den-none 0.32 against den-read
+        // 0.36 ms at C4 / 8, profiles/r04; its H pass reads it)
+        if (asw_disp_pitch(p) != 32) ASWCHK(dev_alloc(&s.den_v, asw_cost_bytes(p)));
         ASWCHK(dev_alloc(&s.den_h, asw_cost_bytes(p)));
     }
     if (sharded) {
@@ -433,8 +435,9 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0], st));
     for (int it = 0; it < p->iters; ++it) {
-        const int dm = !s.den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
-        ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, s.wvl, s.wvr, s.c0, s.c1, s.den_v, dm, st));
+        const int dmv = !s.den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
+        const int dm = !s.den_h ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
+        ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, s.wvl, s.wvr, s.c0, s.c1, s.den_v, dmv, st));
         if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0 + 2 * it + 1], st));
         if (s.otf) ASWCHK(asw_aggregate_pass_otf(p, ASW_DIR_H, s.whl, s.right, s.lut, s.c1, s.c0, s.den_h, dm, st));
         else ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, s.whl, s.whr, s.c1, s.c0, s.den_h, dm, st));

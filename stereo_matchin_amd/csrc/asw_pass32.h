@@ -386,11 +386,15 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
     constexpr int U = pf9_period(T);
     const int W = p->width, H = p->height;
     const int nxb = (W + 2 * NW - 1) / (2 * NW);
-    // row strips: enough blocks for the 256 CUs (NW = 16: one block per CU), strips of
-    // whole U-row chunks, >= 2T rows (the window prologue, U-1 row loads per strip)
-    int nstrip = (int)((512LL * 16 / NW + nxb - 1) / nxb);
+    // row strips: about one block per CU slot (NW = 16: one block per CU, 256 slots) so
+    // the grid is one full round, not a round and a tail; strips of whole U-row chunks,
+    // >= 2T rows (the window prologue, U-1 row loads per strip).  Variant bits 16-19
+    // (asw_tune_set) override the strip count.
+    const int slots = 256 * 16 / NW;
+    int nstrip = (slots + nxb / 2) / nxb;
     const int max_strip = H / (2 * T) > 1 ? H / (2 * T) : 1;
     if (nstrip > max_strip) nstrip = max_strip;
+    if ((g_pass_variant >> 16) & 15) nstrip = (g_pass_variant >> 16) & 15;
     if (nstrip < 1) nstrip = 1;
     const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
     nstrip = (H + rows - 1) / rows;
@@ -429,10 +433,16 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         if (stream) launch_v32<T, NW, DM, kCPStream, NPH>(p, wl, wr, cin, cout, den, st);
         else launch_v32<T, NW, DM, 0, NPH>(p, wl, wr, cin, cout, den, st);
     } else {
-        // segments: the multiple of U nearest W/4 (>= 2 U): at C4 four 480-column
-        // segments per row pair, 2160 waves; the window prologue (U-1 columns) is paid
-        // once per segment
-        int seg = (p->width / 4 + U / 2) / U * U;
+        // segments per row pair: as many as keep the waves within one round of the
+        // 2048 wave slots (8 per CU: two 4-wave blocks of 67 KB LDS) — at C4 three
+        // 640-column segments, 1620 waves (four segments, 2160 waves, left a tail round
+        // of 112 waves); the window prologue (U-1 columns) is paid once per segment.
+        // Variant bits 20-23 (asw_tune_set) override the segment count.
+        const int pairs = (p->height + 1) / 2;
+        int nseg = 2048 / (pairs > 0 ? pairs : 1);
+        if ((g_pass_variant >> 20) & 15) nseg = (g_pass_variant >> 20) & 15;
+        if (nseg < 1) nseg = 1;
+        int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
         if (seg < 2 * U) seg = 2 * U;
         constexpr int NWB = T > 35 ? 2 : 4;
         if (stream) launch_h32<T, NWB, DM, kCPStream, 2>(p, wl, wr, cin, cout, den, st, seg);

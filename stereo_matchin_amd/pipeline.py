@@ -77,7 +77,10 @@ class StereoMatcher:
         self.c1 = K.new_cost(self.p, dev)
         self.den_v = self.den_h = None
         if den_cache and self.p.iters >= 2:
-            self.den_v = K.new_cost(self.p, dev)
+            # a 32-plane shard's V pass recomputes den (k_vpass32: den-none 0.32 against
+            # den-read 0.36 ms at C4 / 8), its H pass reads it (asw_frame.cpp the same)
+            if K.cost_shape(self.p)[2] != 32:
+                self.den_v = K.new_cost(self.p, dev)
             self.den_h = K.new_cost(self.p, dev)
 
     # -- stages ---------------------------------------------------------------
@@ -107,12 +110,13 @@ class StereoMatcher:
         (asw_aggregate_pass_raw) and c0's input content is not used."""
         p = self.p
         for it in range(p.iters):
-            dm = _lib.DEN_NONE if self.den_v is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
+            dmv = _lib.DEN_NONE if self.den_v is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
+            dm = _lib.DEN_NONE if self.den_h is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
             if it == 0 and images is not None:
                 K.asw_vCostAggregation_raw(p, self.wvl, self.wvr, images[0], images[1], out=self.c1, den=self.den_v,
-                                           den_mode=dm)
+                                           den_mode=dmv)
             else:
-                K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1, den=self.den_v, den_mode=dm)
+                K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1, den=self.den_v, den_mode=dmv)
             if events is not None:
                 events.append(("v", _record()))
             if self.otf:
