@@ -1,35 +1,35 @@
-// asw_wta_sweep.hip — asw_WTA (K/asw_wta.cl:12-82) as a row sweep: the left
-// first-argmin and the bresenham target scan of every pixel of a row in ONE pass
-// over the row's volume, with no per-pixel gathers.
+// asw_wta_sweep.hip — asw_WTA (K/asw_wta.cl:12-82) of a whole-range context as a
+// row sweep: the left first-argmin AND the bresenham target scan of every pixel of a
+// row from ONE pass over the row's volume, with no per-pixel gathers.
 //
 // Target scan (K/asw_wta.cl:50-67) of pixel x with left disparity md: for i < md,
 // xq = max(0, x-i), b = md + xq - x, value C[b][y][xq].  For i <= x the points
-// (xq, b) = (x-i, md-i) lie on the diagonal k = xq - b = x - md; for i > x the
-// point clamps to (0, md-x), the diagonal's first point, repeated md-1-x more
-// times.  So the scan of pixel x is the diagonal k = x - md over its points with
-// b >= max(1, -k) and xq <= x, plus those repeats.
-//   The sweep walks x left to right with one state (m1, m2, argmin b) per diagonal,
-// stored at the plane b = x - k the diagonal reaches in column x: lane l holds
-// planes PPL*l .. PPL*l+PPL-1 of the column (one PPL-dword load per lane and
-// column), so from column x to x+1 every state moves up one plane: inside a lane
-// by renaming registers (the unrolled steps rotate which register holds which
-// plane), across lanes by one shuffle of the top plane's state.  Column x then
-// adds its voxel C[b][y][x] to the state at plane b (b >= 1: b = 0 is no target
-// point), and pixel x reads the state at plane md.
-//   Ties: the reference scans i upward with strict '<', so the FIRST i (the largest
-// b) wins; the sweep meets b upward and keeps the LAST with '<='.  The multiset
-// second minimum (m1, m2 of the sequential loop) does not depend on the order; the
-// md-1-x repeats of the first point (0, md-x) enter it as m2 = min(m2, C[md-x][y][0]).
-//   Left scan (K/asw_wta.cl:25-47): each lane scans its PPL planes in order (strict
-// '<'), then a butterfly over the 64 lanes combines (m1, m2, index) with ties to
-// the smaller index (the first argmin).
-// One wave per image row; results of 64 consecutive pixels are gathered into
-// lanes and stored coalesced.  Bit-identical to k_wta_scan<0> (asw_refine.hip).
+// (xq, b) = (x-i, md-i) lie on the diagonal k = xq - b = x - md; for i > x the point
+// clamps to (0, md-x), the diagonal's first point, repeated md-1-x more times.  So
+// the scan of pixel x is diagonal k = x - md over its points with b >= max(1, -k)
+// and xq <= x, plus those repeats.
+//   Diagonal states (m1, m2, argmin b) live in lanes: slot j (= wave*64 + lane, Dp
+// slots) holds the diagonals k = -j (mod Dp), which at column x are at plane
+// b = (x + j) mod Dp.  Column x adds C[b][y][x] to every slot (b = 0 starts the
+// slot's next diagonal, which has no point there), and pixel x reads slot
+// (md - x) mod Dp, whose diagonal is then at plane md.  No state ever moves between
+// lanes: each slot reads its own plane of the column, and a wave's 64 slots read 64
+// consecutive planes.
+//   Ties: the reference scans i upward with strict '<' (the FIRST i, i.e. the largest
+// b, wins); the slots meet b upward and keep the LAST with '<='.  (m1, m2) is the
+// multiset's two smallest whatever the order; the md-1-x repeats of the first point
+// enter as m2 = min(m2, C[md-x][y][0]).
+//   Left scan (K/asw_wta.cl:25-47): lane = pixel, wave w scans planes [64w, 64w+64)
+// of the tile's 64 pixels in order with strict '<'; the NW partials combine in plane
+// order (ties to the smaller index: the first argmin).
+// Block = NW = Dp/64 waves, one image row; the row is staged 64 columns at a time in
+// LDS ([column][plane], pitch Dp+4: lane-per-pixel ds_read_b128 and slot ds_read_b32
+// both conflict-free), the next tile loaded into registers while the current one is
+// swept.  Bit-identical to k_wta_scan<0> (asw_refine.hip).
 #include <hip/hip_runtime.h>
 
 #include <climits>
 #include <cstdint>
-#include <type_traits>
 
 #include "asw_common.h"
 
@@ -37,186 +37,179 @@ namespace asw {
 namespace {
 
 constexpr float kSent = 100000.0f;  // K/asw_wta.cl:25-26
+constexpr int kTC = 64;             // columns per tile
 
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F &&f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        sfor<B + 1, E>(f);
-    }
+__device__ __forceinline__ float lane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
-struct Top2 {
-    float m1, m2;
-    int idx;
-};
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_wta_tile(const float *__restrict__ cost, int W, int H, int D,
+                                                      int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
+                                                      int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
+                                                      uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar) {
+    using f4 = float __attribute__((ext_vector_type(4)));
+    constexpr int Dp = 64 * NW;
+    constexpr int PITCH = Dp + 4;
+    constexpr int NQ = Dp / 4;                   // float4 per column
+    constexpr int SPT = kTC * NQ / (NW * 64);    // staged float4 per thread (16)
+    __shared__ float tile[kTC * PITCH];
+    __shared__ float part_m1[NW][64], part_m2[NW][64];
+    __shared__ int part_idx[NW][64];
 
-// combine two partial scans of disjoint plane sets: first argmin (ties -> smaller
-// index), multiset second minimum
-__device__ __forceinline__ Top2 combine(const Top2 &a, float om1, float om2, int oidx) {
-    Top2 r;
-    r.m2 = fminf(fmaxf(a.m1, om1), fminf(a.m2, om2));
-    const bool take = (om1 < a.m1) || (om1 == a.m1 && oidx < a.idx);
-    r.m1 = take ? om1 : a.m1;
-    r.idx = take ? oidx : a.idx;
-    return r;
-}
-
-// PPL planes per lane (Dp = 64 PPL); PF columns of loads in flight
-template <int PPL, int PF>
-__global__ __launch_bounds__(64) void k_wta_sweep(const float *__restrict__ cost, int W, int H, int D,
-                                                  int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
-                                                  int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
-                                                  uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar) {
-    constexpr int Dp = 64 * PPL;
-    static_assert(PF % PPL == 0, "register rotation period");
     const int y = blockIdx.x;
     if (y >= H) return;
-    const int lane = threadIdx.x;
-    const float *row = cost + (long long)y * W * Dp + PPL * lane;
-    auto load = [&](int x, float (&v)[PPL]) __attribute__((always_inline)) {
-        const float *pp = row + (long long)min(x, W - 1) * Dp;
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) v[j] = pp[j];
-    };
-    float ring[PF][PPL];
-#pragma unroll
-    for (int s = 0; s < PF; ++s) load(s, ring[s]);
-    float col0[PPL];  // column 0: the clamped first points of the negative diagonals
-#pragma unroll
-    for (int j = 0; j < PPL; ++j) col0[j] = ring[0][j];
-
-    // diagonal states; physical register p holds plane slot (p + x) mod PPL at column x
-    float sm1[PPL], sm2[PPL];
-    int sb[PPL];
-#pragma unroll
-    for (int j = 0; j < PPL; ++j) {
-        sm1[j] = kSent;
-        sm2[j] = kSent;
-        sb[j] = -1;
-    }
-    // per-pixel results gathered into lane (x & 63)
-    int o_md = 0, o_tb = 0;
-    float o_m1 = kSent, o_m2 = kSent, o_t1 = kSent, o_t2 = kSent;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = wave * 64 + lane;  // diagonal slot
+    const float *rowp = cost + (long long)y * W * Dp;
     const long long rbase = (long long)y * W;
-    auto flush = [&](int xbase, int n) __attribute__((always_inline)) {
-        if (lane < n) {
-            const long long p = rbase + xbase + lane;
-            d_ref[p] = o_md;
+
+    f4 stage[SPT];
+    auto load_tile = [&](int x0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int f = (int)threadIdx.x + i * NW * 64;
+            const int c = f / NQ, g = f - c * NQ;
+            stage[i] = *reinterpret_cast<const f4 *>(rowp + (long long)min(x0 + c, W - 1) * Dp + 4 * g);
+        }
+    };
+    auto write_tile = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int f = (int)threadIdx.x + i * NW * 64;
+            const int c = f / NQ, g = f - c * NQ;
+            *reinterpret_cast<f4 *>(&tile[c * PITCH + 4 * g]) = stage[i];
+        }
+    };
+
+    load_tile(0);
+    write_tile();
+    __syncthreads();
+    const float first_v = tile[j];  // C[j][y][0]: the first point of slot j's diagonal k = -j
+    float sm1 = kSent, sm2 = kSent;
+    int sb = -1;
+
+    for (int x0 = 0; x0 < W; x0 += kTC) {
+        const int nc = min(kTC, W - x0);
+        if (x0 + kTC < W) load_tile(x0 + kTC);  // in flight while this tile is swept
+        // ---- left scan, lane = pixel x0 + lane, this wave's 64 planes
+        {
+            float m1 = kSent, m2 = kSent;
+            int idx = INT_MAX;
+            const float *pp = &tile[lane * PITCH + 64 * wave];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const f4 v = *reinterpret_cast<const f4 *>(pp + 4 * q);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int d = 64 * wave + 4 * q + e;
+                    const float c = d < D ? v[e] : __builtin_inff();
+                    m2 = c < m2 ? c : m2;
+                    idx = c < m1 ? d : idx;
+                    m2 = c < m1 ? m1 : m2;
+                    m1 = c < m1 ? c : m1;
+                }
+            }
+            part_m1[wave][lane] = m1;
+            part_m2[wave][lane] = m2;
+            part_idx[wave][lane] = idx;
+        }
+        __syncthreads();
+        float M1 = part_m1[0][lane], M2 = part_m2[0][lane];
+        int MI = part_idx[0][lane];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {  // higher planes: ties keep the smaller index
+            const float om1 = part_m1[w][lane], om2 = part_m2[w][lane];
+            const int oi = part_idx[w][lane];
+            M2 = fminf(fmaxf(M1, om1), fminf(M2, om2));
+            const bool take = om1 < M1;
+            M1 = take ? om1 : M1;
+            MI = take ? oi : MI;
+        }
+        const int md_lane = MI == INT_MAX ? 0 : MI;
+        if (wave == 0 && lane < nc) {
+            const long long p = rbase + x0 + lane;
+            d_ref[p] = md_lane;
+            conf_ref[p] = (M2 - M1) / M2;
+            if (code_ref) code_ref[p] = (uint8_t)code_u8(md_lane, D);
+        }
+        // ---- diagonal sweep of the tile's columns
+        float o_t1 = kSent, o_t2 = kSent;
+        int o_tb = 0;
+        bool mine = false;
+        for (int c = 0; c < nc; ++c) {
+            const int x = x0 + c;
+            const int b = (x + j) % Dp;
+            if (b == 0) {  // slot j starts diagonal k = x (no point at b = 0)
+                sm1 = kSent;
+                sm2 = kSent;
+                sb = -1;
+            } else {
+                const float t = b < D ? tile[c * PITCH + b] : __builtin_inff();
+                const bool le = t <= sm1;
+                sm2 = le ? sm1 : fminf(sm2, t);
+                sb = le ? b : sb;
+                sm1 = le ? t : sm1;
+            }
+            const int md = __builtin_amdgcn_readlane(md_lane, c);
+            if (md >= 1) {
+                const int qs = ((md - x) % Dp + Dp) % Dp;  // slot of diagonal x - md
+                if ((qs >> 6) == wave) {
+                    const int ql = qs & 63;
+                    const float t1 = lane_f(sm1, ql);
+                    float t2 = lane_f(sm2, ql);
+                    const int tb = __builtin_amdgcn_readlane(sb, ql);
+                    if (md - x >= 2) t2 = fminf(t2, lane_f(first_v, ql));  // the clamped repeats
+                    if (lane == c) {
+                        o_t1 = t1;
+                        o_t2 = t2;
+                        o_tb = tb;
+                        mine = true;
+                    }
+                }
+            } else if (wave == 0 && lane == c) {  // md = 0: no target scan
+                mine = true;
+            }
+        }
+        if (mine && lane < nc) {
+            const long long p = rbase + x0 + lane;
             d_tar[p] = o_tb;
-            conf_ref[p] = (o_m2 - o_m1) / o_m2;
             conf_tar[p] = (o_t2 - o_t1) / o_t2;
-            if (code_ref) code_ref[p] = (uint8_t)code_u8(o_md, D);
             if (code_tar) code_tar[p] = (uint8_t)code_u8(o_tb, D);
         }
-    };
-
-    auto step = [&](auto sc, int x) __attribute__((always_inline)) {
-        constexpr int s = decltype(sc)::value;
-        float v[PPL];
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) v[j] = ring[s][j];
-        load(x + PF, ring[s]);
-        // ---- left scan of column x
-        Top2 t{kSent, kSent, INT_MAX};
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) {
-            const int d = PPL * lane + j;
-            const float c = d < D ? v[j] : __builtin_inff();
-            t.m2 = c < t.m2 ? c : t.m2;
-            t.idx = c < t.m1 ? d : t.idx;
-            t.m2 = c < t.m1 ? t.m1 : t.m2;
-            t.m1 = c < t.m1 ? c : t.m1;
+        __syncthreads();  // every read of this tile is done
+        if (x0 + kTC < W) {
+            write_tile();
+            __syncthreads();
         }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) t = combine(t, __shfl_xor(t.m1, o), __shfl_xor(t.m2, o), __shfl_xor(t.idx, o));
-        const int md = __builtin_amdgcn_readfirstlane(t.idx == INT_MAX ? 0 : t.idx);
-        // ---- diagonal states: move up one plane (column x-1 -> x).  The physical
-        // register of the top plane slot becomes plane slot 0, fed by the lane below.
-        // (x = s mod PPL: the sweep runs in PF-column periods, PF a multiple of PPL)
-        constexpr int ptop = ((-s) % PPL + PPL) % PPL;  // top slot at column x-1 = slot 0 at column x
-        {
-            const float a = __shfl_up(sm1[ptop], 1), b2 = __shfl_up(sm2[ptop], 1);
-            const int bi = __shfl_up(sb[ptop], 1);
-            sm1[ptop] = lane == 0 ? kSent : a;
-            sm2[ptop] = lane == 0 ? kSent : b2;
-            sb[ptop] = lane == 0 ? -1 : bi;
-        }
-        // ---- add column x's voxels: plane slot j lives in physical ((j - s) mod PPL)
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) {
-            const int p = ((j - s) % PPL + PPL) % PPL;
-            const int b = PPL * lane + j;
-            const float c = (b >= 1 && b < D) ? v[j] : __builtin_inff();
-            const bool le = c <= sm1[p];
-            sm2[p] = le ? sm1[p] : fminf(sm2[p], c);
-            sb[p] = le ? b : sb[p];
-            sm1[p] = le ? c : sm1[p];
-        }
-        // ---- the target scan of pixel x: the state at plane md
-        float t1 = kSent, t2 = kSent;
-        int tb = md;
-        if (md >= 1) {
-            const int ln = md / PPL, slot = md - ln * PPL;
-            const int p = ((slot - s) % PPL + PPL) % PPL;
-            float a1 = sm1[0], a2 = sm2[0];
-            int ab = sb[0];
-#pragma unroll
-            for (int q = 1; q < PPL; ++q) {
-                a1 = p == q ? sm1[q] : a1;
-                a2 = p == q ? sm2[q] : a2;
-                ab = p == q ? sb[q] : ab;
-            }
-            t1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a1), ln));
-            t2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a2), ln));
-            tb = __builtin_amdgcn_readlane(ab, ln);
-            if (md - x >= 2) {  // the repeats of the clamped first point (0, md - x)
-                const int b0 = md - x, l0 = b0 / PPL, j0 = b0 - l0 * PPL;
-                float c0 = col0[0];
-#pragma unroll
-                for (int q = 1; q < PPL; ++q) c0 = j0 == q ? col0[q] : c0;
-                const float v0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, c0), l0));
-                t2 = fminf(t2, v0);
-            }
-        }
-        if (lane == (x & 63)) {
-            o_md = md;
-            o_m1 = t.m1;
-            o_m2 = t.m2;
-            o_tb = tb;
-            o_t1 = t1;
-            o_t2 = t2;
-        }
-        if ((x & 63) == 63) flush(x - 63, 64);
-    };
-    int x = 0;
-    for (; x + PF <= W; x += PF) sfor<0, PF>([&](auto sc) __attribute__((always_inline)) { step(sc, x + decltype(sc)::value); });
-    for (int xr = x; xr < W; xr += PF) {  // the last partial period
-        sfor<0, PF>([&](auto sc) __attribute__((always_inline)) {
-            if (xr + decltype(sc)::value < W) step(sc, xr + decltype(sc)::value);
-        });
     }
-    if (W & 63) flush(W - (W & 63), W & 63);
 }
 
 }  // namespace
 
-// asw_WTA of a whole-range context (d_begin = 0) through the row sweep; Dp = 64..256.
-// ASW_E_UNSUPPORTED for other pitches (the caller then runs k_wta_scan).
+// asw_WTA of a whole-range context through the row sweep; Dp = 64, 128 or 256
+// (ASW_E_UNSUPPORTED otherwise: the caller then runs k_wta_scan).
 int launch_wta_sweep(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
                      float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, hipStream_t st) {
     const int Dp = asw_disp_pitch(p);
-    const dim3 grid((unsigned)p->height), block(64);
-#define ASW_SWEEP(PPL, PF)                                                                                         \
-    hipLaunchKernelGGL((k_wta_sweep<PPL, PF>), grid, block, 0, st, cost, p->width, p->height, p->ndisp, d_ref,    \
-                       conf_ref, d_tar, conf_tar, code_ref, code_tar)
+    const dim3 grid((unsigned)p->height);
     switch (Dp) {
-        case 64: ASW_SWEEP(1, 16); break;
-        case 128: ASW_SWEEP(2, 16); break;
-        case 256: ASW_SWEEP(4, 16); break;
-        default: return ASW_E_UNSUPPORTED;
+        case 64:
+            hipLaunchKernelGGL(k_wta_tile<1>, grid, dim3(64), 0, st, cost, p->width, p->height, p->ndisp, d_ref,
+                               conf_ref, d_tar, conf_tar, code_ref, code_tar);
+            break;
+        case 128:
+            hipLaunchKernelGGL(k_wta_tile<2>, grid, dim3(128), 0, st, cost, p->width, p->height, p->ndisp, d_ref,
+                               conf_ref, d_tar, conf_tar, code_ref, code_tar);
+            break;
+        case 256:
+            hipLaunchKernelGGL(k_wta_tile<4>, grid, dim3(256), 0, st, cost, p->width, p->height, p->ndisp, d_ref,
+                               conf_ref, d_tar, conf_tar, code_ref, code_tar);
+            break;
+        default:
+            return ASW_E_UNSUPPORTED;
     }
-#undef ASW_SWEEP
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_hip_error(e);
