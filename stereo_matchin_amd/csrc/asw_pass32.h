@@ -209,8 +209,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
 // ---------------------------------------------------------------------------
 constexpr int h32_batch(int T) { return tap_pitch(T) / 4 * 8 <= 64 * 4 ? 4 : 2; }
 
-template <int T, int NWB, int DM, int CP, int NPH>
-__global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(2))) void k_hpass32(
+// RING16: right ring of a multiple of 16 entries (conflict-free across the wrap) or
+// the minimal 32 + 2K (a 2-way conflict where a read wraps; less LDS, more waves)
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2>
+__global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_hpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
     float *__restrict__ den, int W, int H, int d_begin, int nseg, int seg_len, int npairs, int pairs_per_xcd) {
     constexpr int R = T / 2;
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(2))) v
     constexpr int P = U - T;
     constexpr int KD = 4;  // den prefetch ring (steps)
     constexpr int K = h32_batch(T);
-    constexpr int RING = (32 + 2 * K + 15) / 16 * 16;  // right entries per row (multiple of 16: conflict-free wrap)
+    constexpr int RING = RING16 ? (32 + 2 * K + 15) / 16 * 16 : 32 + 2 * K;  // right entries per row
     constexpr int LRING = 2 * K + 2;                   // left entries per row
     constexpr int ROWE = RING + LRING;                 // ring entries per row
     static_assert(U % K == 0, "the batch top must be a compile-time step");
@@ -405,7 +407,7 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
                      CP == kCPStream);
 }
 
-template <int T, int NWB, int DM, int CP, int NPH>
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2>
 void launch_h32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
                 hipStream_t st, int seg_len) {
     const int W = p->width, H = p->height;
@@ -413,9 +415,19 @@ void launch_h32(const asw_params *p, const float *wl, const float *wr, const flo
     const int npairs = (H + 1) / 2 * nseg;  // work items: (row pair, segment)
     const int per_xcd = (npairs + 7) / 8;
     const int blocks_per_xcd = (per_xcd + NWB - 1) / NWB;
-    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH>), dim3(8 * blocks_per_xcd), dim3(NWB * 64), 0, st, wl, wr, cin,
-                       cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd);
-    note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T, NWB == 4 ? "NWB=4" : "NWB=2", CP == kCPStream);
+    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE>), dim3(8 * blocks_per_xcd), dim3(NWB * 64), 0, st,
+                       wl, wr, cin, cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd);
+    note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T,
+                     NPH == 4 ? "NWB=1,NPH=4" : NWB == 4 ? "NWB=4" : "NWB=2", CP == kCPStream);
+}
+
+inline int finish32() {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_hip_error(e);
+        return ASW_E_HIP;
+    }
+    return ASW_OK;
 }
 
 template <int T, int DM>
@@ -438,22 +450,29 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         // 640-column segments, 1620 waves (four segments, 2160 waves, left a tail round
         // of 112 waves); the window prologue (U-1 columns) is paid once per segment.
         // Variant bits 20-23 (asw_tune_set) override the segment count.
+        // Variant bit 24: the T <= 35 kernel in 4 weight phases with the minimal right
+        // ring (<= 168 VGPRs, 14.4 KB LDS per wave: 11 waves per CU against 8).
+        const bool lean = T <= 35 && (g_pass_variant & (1 << 24));
+        const int slots = lean ? 2816 : 2048;
         const int pairs = (p->height + 1) / 2;
-        int nseg = 2048 / (pairs > 0 ? pairs : 1);
+        int nseg = slots / (pairs > 0 ? pairs : 1);
         if ((g_pass_variant >> 20) & 15) nseg = (g_pass_variant >> 20) & 15;
         if (nseg < 1) nseg = 1;
         int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
         if (seg < 2 * U) seg = 2 * U;
         constexpr int NWB = T > 35 ? 2 : 4;
+        if constexpr (T <= 35) {
+            if (lean) {
+                // (one-wave blocks: 14.4 KB of LDS each, so 11 fit a CU)
+                if (stream) launch_h32<T, 1, DM, kCPStream, 4, false, 3>(p, wl, wr, cin, cout, den, st, seg);
+                else launch_h32<T, 1, DM, 0, 4, false, 3>(p, wl, wr, cin, cout, den, st, seg);
+                return finish32();
+            }
+        }
         if (stream) launch_h32<T, NWB, DM, kCPStream, 2>(p, wl, wr, cin, cout, den, st, seg);
         else launch_h32<T, NWB, DM, 0, 2>(p, wl, wr, cin, cout, den, st, seg);
     }
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_hip_error(e);
-        return ASW_E_HIP;
-    }
-    return ASW_OK;
+    return finish32();
 }
 
 }  // namespace agg

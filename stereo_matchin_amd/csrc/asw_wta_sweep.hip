@@ -11,10 +11,10 @@
 //   Diagonal states (m1, m2, argmin b) live in lanes: slot j (= wave*64 + lane, Dp
 // slots) holds the diagonals k = -j (mod Dp), which at column x are at plane
 // b = (x + j) mod Dp.  Column x adds C[b][y][x] to every slot (b = 0 starts the
-// slot's next diagonal, which has no point there), and pixel x reads slot
-// (md - x) mod Dp, whose diagonal is then at plane md.  No state ever moves between
-// lanes: each slot reads its own plane of the column, and a wave's 64 slots read 64
-// consecutive planes.
+// slot's next diagonal, which has no point there), and pixel x takes the state of
+// the one slot whose plane is then md(x) (slot (md - x) mod Dp), which writes it to
+// LDS.  No state ever moves between lanes: each slot reads its own plane of the
+// column, and a wave's 64 slots read 64 consecutive planes.
 //   Ties: the reference scans i upward with strict '<' (the FIRST i, i.e. the largest
 // b, wins); the slots meet b upward and keep the LAST with '<='.  (m1, m2) is the
 // multiset's two smallest whatever the order; the md-1-x repeats of the first point
@@ -39,10 +39,6 @@ namespace {
 constexpr float kSent = 100000.0f;  // K/asw_wta.cl:25-26
 constexpr int kTC = 64;             // columns per tile
 
-__device__ __forceinline__ float lane_f(float v, int l) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-}
-
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void k_wta_tile(const float *__restrict__ cost, int W, int H, int D,
                                                       int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
@@ -56,6 +52,8 @@ __global__ __launch_bounds__(NW * 64) void k_wta_tile(const float *__restrict__ 
     __shared__ float tile[kTC * PITCH];
     __shared__ float part_m1[NW][64], part_m2[NW][64];
     __shared__ int part_idx[NW][64];
+    __shared__ float res_t1[kTC], res_t2[kTC];  // the target scan of each pixel of the tile
+    __shared__ int res_tb[kTC];
 
     const int y = blockIdx.x;
     if (y >= H) return;
@@ -134,49 +132,56 @@ __global__ __launch_bounds__(NW * 64) void k_wta_tile(const float *__restrict__ 
             conf_ref[p] = (M2 - M1) / M2;
             if (code_ref) code_ref[p] = (uint8_t)code_u8(md_lane, D);
         }
-        // ---- diagonal sweep of the tile's columns
-        float o_t1 = kSent, o_t2 = kSent;
-        int o_tb = 0;
-        bool mine = false;
-        for (int c = 0; c < nc; ++c) {
-            const int x = x0 + c;
-            const int b = (x + j) % Dp;
-            if (b == 0) {  // slot j starts diagonal k = x (no point at b = 0)
-                sm1 = kSent;
-                sm2 = kSent;
-                sb = -1;
-            } else {
-                const float t = b < D ? tile[c * PITCH + b] : __builtin_inff();
-                const bool le = t <= sm1;
-                sm2 = le ? sm1 : fminf(sm2, t);
-                sb = le ? b : sb;
-                sm1 = le ? t : sm1;
+        // ---- diagonal sweep of the tile's columns.  Pixel x's target scan is the slot
+        // whose plane at column x is md(x) (slot (md - x) mod Dp): that lane alone sees
+        // b == md and records its state for the pixel (res_*; md = 0: the defaults).
+        if (wave == 0) {
+            res_t1[lane] = kSent;
+            res_t2[lane] = kSent;
+            res_tb[lane] = 0;
+        }
+        __syncthreads();
+        constexpr int CH = 16;  // columns per batch of tile reads
+        for (int c0 = 0; c0 < nc; c0 += CH) {
+            float tv[CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const int b = (x0 + c0 + k + j) & (Dp - 1);
+                tv[k] = tile[(c0 + k) * PITCH + b];
             }
-            const int md = __builtin_amdgcn_readlane(md_lane, c);
-            if (md >= 1) {
-                const int qs = ((md - x) % Dp + Dp) % Dp;  // slot of diagonal x - md
-                if ((qs >> 6) == wave) {
-                    const int ql = qs & 63;
-                    const float t1 = lane_f(sm1, ql);
-                    float t2 = lane_f(sm2, ql);
-                    const int tb = __builtin_amdgcn_readlane(sb, ql);
-                    if (md - x >= 2) t2 = fminf(t2, lane_f(first_v, ql));  // the clamped repeats
-                    if (lane == c) {
-                        o_t1 = t1;
-                        o_t2 = t2;
-                        o_tb = tb;
-                        mine = true;
-                    }
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const int c = c0 + k;
+                if (c >= nc) break;  // uniform
+                const int x = x0 + c;
+                const int b = (x + j) & (Dp - 1);
+                if (b == 0) {  // slot j starts diagonal k = x (no point at b = 0)
+                    sm1 = kSent;
+                    sm2 = kSent;
+                    sb = -1;
+                } else {
+                    const float t = b < D ? tv[k] : __builtin_inff();
+                    const bool le = t <= sm1;
+                    sm2 = le ? sm1 : fminf(sm2, t);
+                    sb = le ? b : sb;
+                    sm1 = le ? t : sm1;
                 }
-            } else if (wave == 0 && lane == c) {  // md = 0: no target scan
-                mine = true;
+                const int md = __builtin_amdgcn_readlane(md_lane, c);
+                if (b == md && md >= 1) {  // one lane of the block, if any
+                    res_t1[c] = sm1;
+                    res_t2[c] = md - x >= 2 ? fminf(sm2, first_v) : sm2;  // the clamped repeats
+                    res_tb[c] = sb;
+                }
             }
         }
-        if (mine && lane < nc) {
+        __syncthreads();
+        if (wave == 0 && lane < nc) {
             const long long p = rbase + x0 + lane;
-            d_tar[p] = o_tb;
-            conf_tar[p] = (o_t2 - o_t1) / o_t2;
-            if (code_tar) code_tar[p] = (uint8_t)code_u8(o_tb, D);
+            const float t1 = res_t1[lane], t2 = res_t2[lane];
+            const int tb = res_tb[lane];
+            d_tar[p] = tb;
+            conf_tar[p] = (t2 - t1) / t2;
+            if (code_tar) code_tar[p] = (uint8_t)code_u8(tb, D);
         }
         __syncthreads();  // every read of this tile is done
         if (x0 + kTC < W) {
