@@ -450,12 +450,13 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         // 640-column segments, 1620 waves (four segments, 2160 waves, left a tail round
         // of 112 waves); the window prologue (U-1 columns) is paid once per segment.
         // Variant bits 20-23 (asw_tune_set) override the segment count.
-        // Variant bit 24: the T <= 35 kernel in 4 weight phases with the minimal right
-        // ring (<= 168 VGPRs, 14.4 KB LDS per wave: 11 waves per CU against 8).
-        const bool lean = T <= 35 && (g_pass_variant & (1 << 24));
-        const int slots = lean ? 2816 : 2048;
+        // T <= 35: the "lean" form, 4 weight phases and the minimal right ring (138
+        // VGPRs, 14.4 KB of LDS per one-wave block: up to 11 waves per CU against 8):
+        // C4 / 8 den-read 0.326 against 0.358 ms (profiles/r04/pass32_h_r09e.log).  Variant
+        // bit 24 selects the 4-wave-block form instead.
+        const bool lean = T <= 35 && !(g_pass_variant & (1 << 24));
         const int pairs = (p->height + 1) / 2;
-        int nseg = slots / (pairs > 0 ? pairs : 1);
+        int nseg = (2048 + pairs / 2) / (pairs > 0 ? pairs : 1);  // C4: 4 segments of 480 columns
         if ((g_pass_variant >> 20) & 15) nseg = (g_pass_variant >> 20) & 15;
         if (nseg < 1) nseg = 1;
         int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;

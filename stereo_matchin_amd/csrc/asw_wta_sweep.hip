@@ -93,25 +93,45 @@ __global__ __launch_bounds__(NW * 64) void k_wta_tile(const float *__restrict__ 
         if (x0 + kTC < W) load_tile(x0 + kTC);  // in flight while this tile is swept
         // ---- left scan, lane = pixel x0 + lane, this wave's 64 planes
         {
-            float m1 = kSent, m2 = kSent;
-            int idx = INT_MAX;
+            // four independent sequential scans of 16 planes each (latency: the chains
+            // interleave), combined in plane order
+            float m1[4], m2[4];
+            int idx[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                m1[h] = kSent;
+                m2[h] = kSent;
+                idx[h] = INT_MAX;
+            }
             const float *pp = &tile[lane * PITCH + 64 * wave];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const f4 v = *reinterpret_cast<const f4 *>(pp + 4 * q);
+            for (int q = 0; q < 4; ++q) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int d = 64 * wave + 4 * q + e;
-                    const float c = d < D ? v[e] : __builtin_inff();
-                    m2 = c < m2 ? c : m2;
-                    idx = c < m1 ? d : idx;
-                    m2 = c < m1 ? m1 : m2;
-                    m1 = c < m1 ? c : m1;
+                for (int h = 0; h < 4; ++h) {
+                    const f4 v = *reinterpret_cast<const f4 *>(pp + 16 * h + 4 * q);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int d = 64 * wave + 16 * h + 4 * q + e;
+                        const float c = d < D ? v[e] : __builtin_inff();
+                        m2[h] = c < m2[h] ? c : m2[h];
+                        idx[h] = c < m1[h] ? d : idx[h];
+                        m2[h] = c < m1[h] ? m1[h] : m2[h];
+                        m1[h] = c < m1[h] ? c : m1[h];
+                    }
                 }
             }
-            part_m1[wave][lane] = m1;
-            part_m2[wave][lane] = m2;
-            part_idx[wave][lane] = idx;
+            float a1 = m1[0], a2 = m2[0];
+            int ai = idx[0];
+#pragma unroll
+            for (int h = 1; h < 4; ++h) {  // higher planes: ties keep the smaller index
+                a2 = fminf(fmaxf(a1, m1[h]), fminf(a2, m2[h]));
+                const bool take = m1[h] < a1;
+                a1 = take ? m1[h] : a1;
+                ai = take ? idx[h] : ai;
+            }
+            part_m1[wave][lane] = a1;
+            part_m2[wave][lane] = a2;
+            part_idx[wave][lane] = ai;
         }
         __syncthreads();
         float M1 = part_m1[0][lane], M2 = part_m2[0][lane];
@@ -152,25 +172,26 @@ __global__ __launch_bounds__(NW * 64) void k_wta_tile(const float *__restrict__ 
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
                 const int c = c0 + k;
-                if (c >= nc) break;  // uniform
-                const int x = x0 + c;
-                const int b = (x + j) & (Dp - 1);
-                if (b == 0) {  // slot j starts diagonal k = x (no point at b = 0)
-                    sm1 = kSent;
-                    sm2 = kSent;
-                    sb = -1;
-                } else {
-                    const float t = b < D ? tv[k] : __builtin_inff();
-                    const bool le = t <= sm1;
-                    sm2 = le ? sm1 : fminf(sm2, t);
-                    sb = le ? b : sb;
-                    sm1 = le ? t : sm1;
-                }
-                const int md = __builtin_amdgcn_readlane(md_lane, c);
-                if (b == md && md >= 1) {  // one lane of the block, if any
-                    res_t1[c] = sm1;
-                    res_t2[c] = md - x >= 2 ? fminf(sm2, first_v) : sm2;  // the clamped repeats
-                    res_tb[c] = sb;
+                if (c < nc) {  // uniform (the last tile of a row may be partial)
+                    const int x = x0 + c;
+                    const int b = (x + j) & (Dp - 1);
+                    if (b == 0) {  // slot j starts diagonal k = x (no point at b = 0)
+                        sm1 = kSent;
+                        sm2 = kSent;
+                        sb = -1;
+                    } else {
+                        const float t = b < D ? tv[k] : __builtin_inff();
+                        const bool le = t <= sm1;
+                        sm2 = le ? sm1 : fminf(sm2, t);
+                        sb = le ? b : sb;
+                        sm1 = le ? t : sm1;
+                    }
+                    const int md = __builtin_amdgcn_readlane(md_lane, c);
+                    if (b == md && md >= 1) {  // one lane of the block, if any
+                        res_t1[c] = sm1;
+                        res_t2[c] = md - x >= 2 ? fminf(sm2, first_v) : sm2;  // the clamped repeats
+                        res_tb[c] = sb;
+                    }
                 }
             }
         }

@@ -8,6 +8,7 @@
 #   bench:ARGS  python bench.py ARGS  ('+'-separated, e.g. bench:--workload+c5+--steps+3)
 #   prof        rocprofv3 --kernel-trace --stats of bench.py --no-cpu
 #   prof:ARGS   the same with bench.py ARGS
+#   profpy:ARGS rocprofv3 --kernel-trace --stats of python3 ARGS (a tool script)
 #   pass        tools/pass_bench.py (den modes, default variant)
 #   pmc         rocprofv3 --pmc counter sets (one run each) over tools/pass_bench.py
 #   calib       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over tools/ubench/fetch_calib
@@ -63,6 +64,10 @@ for step in "$@"; do
         prof)
             run 600 "prof_$TAG" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                 python3 bench.py --steps 5 --warmup 1 --no-cpu $args ;;
+        profpy)  # rocprofv3 kernel stats of any python script: profpy:tools/x.py+--arg+v
+            nprof=$((${nprof:-0} + 1))
+            run 600 "profpy${nprof}_$TAG" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profpy$nprof" -o run -- \
+                python3 $args ;;
         pass) run 600 "pass_$TAG${arg:+_${args// /_}}" $PY tools/pass_bench.py --reps 6 --den ${args:---variants 0} ;;
         pmc)
             i=0

@@ -33,7 +33,8 @@ def key_of(name: str):
         return None
     args = [a.strip() for a in m.group(2).split(",")]
     dm = int(args[3]) if m.group(1) == "k_hpass9" else int(args[2])
-    return f"{m.group(1)}<T={args[0]},{DM[dm]}>"
+    otf = m.group(1) == "k_hpass11" and len(args) > 5 and args[5] == "true"  # right weights on the fly
+    return f"{m.group(1)}{'_otf' if otf else ''}<T={args[0]},{DM[dm]}>"
 
 
 def main():
