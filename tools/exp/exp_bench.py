@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--v", action="store_true", help="V-pass experiments")
     ap.add_argument("--lib", default="libexp.so")
     ap.add_argument("--c5", action="store_true", help="C5 block-shape experiments (T = 51)")
+    ap.add_argument("--c5s", default="", help="C5 V strip experiments: nstrip:kbi,... (libexp_c5s.so)")
     ap.add_argument("--c5libs", default="libexp_c5_1641.so:1641")
     ap.add_argument("--vexps", default="prod_read,v12_read,prod_none")
     ap.add_argument("--h", action="store_true", help="H-pass experiments")
@@ -57,8 +58,14 @@ def main():
         # V den-read at T = 51: production pass against k_vpass10 shapes, one library each
         # (--c5libs lib:shape,...; shape = NW*100 + NPH*10 + RB)
         cur = torch.cuda.current_stream().cuda_stream
-        exps = [(lb, int(sh)) for lb, sh in (x.split(":") for x in args.c5libs.split(","))]
+        exps = [(lb, int(sh)) for lb, sh in (x.split(":") for x in args.c5libs.split(","))] if not args.c5s else []
         libs = {lb: ctypes.CDLL(os.path.join(ROOT, "tools", "exp", lb)) for lb, _ in exps}
+        if args.c5s:  # (nstrip, kbi) pairs through libexp_c5s.so, shape code = nstrip * 10 + kbi
+            ls = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp_c5s.so"))
+            for x in args.c5s.split(","):
+                ns, kb = (int(v) for v in x.split(":"))
+                libs[f"s{ns}:{kb}"] = ls
+                exps.append((f"s{ns}:{kb}", ns * 10 + kb))
         den_d = torch.empty_like(cin)
         ref_d = torch.empty_like(cin)
         K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=ref_d, den=den_d, den_mode=1)
@@ -74,6 +81,9 @@ def main():
                 e0.record()
                 if lb is None:
                     K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=den_d, den_mode=2)
+                elif lb.startswith("s"):
+                    assert libs[lb].exp_c5s(sh // 10, sh % 10, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(den_d),
+                                            ctypes.c_void_p(cur)) == 0
                 else:
                     assert libs[lb].exp_c5(0, sh, 2, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(den_d),
                                            ctypes.c_void_p(cur)) == 0

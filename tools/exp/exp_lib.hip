@@ -79,3 +79,31 @@ extern "C" int exp_vpx(int dm, const asw_params *p, const float *wl, const float
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
+
+#ifdef EXP_C5S
+// C5 (T = 51) V den-read with an explicit row-strip count and dispatch order (round 4):
+// whether strips short enough for the Infinity Cache to hold a strip's support rows
+// while all plane blocks pass over it (the plane blocks re-fetch the support rows:
+// 81 GB per launch against 54 compulsory, profiles/r04/pmc_c5_r09d.json) pay for their
+// window prologue.  kbi = 1: the plane blocks of a column group adjacent in dispatch.
+extern "C" int exp_c5s(int nstrip, int kbi, const asw_params *p, const float *wl, const float *wr, const float *cin,
+                       float *cout, float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (p->taps != 51) return -4;
+    constexpr int T = 51, NW = 12;
+    constexpr int U = pf9_period(T);
+    const int W = p->width, H = p->height, Dp = asw_disp_pitch(p), nkb = Dp / 64, nxb = (W + NW - 1) / NW;
+    const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
+    nstrip = (H + rows - 1) / rows;
+    const int per_xcd = (nxb + 7) / 8;
+    if (kbi)
+        hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, 2, kCPStream, kCPStream, 2, 4, true, 3>),
+                           dim3(8 * per_xcd * nkb * nstrip), dim3(NW * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp,
+                           p->d_begin, rows, nxb, nstrip, per_xcd);
+    else
+        hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, 2, kCPStream, kCPStream, 2, 4, false, 3>),
+                           dim3(8 * per_xcd * nkb * nstrip), dim3(NW * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp,
+                           p->d_begin, rows, nxb, nstrip, per_xcd);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+#endif
