@@ -165,6 +165,26 @@ int asw_pass_otf_supported(const asw_params *p, int dir);
 int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
                            const uint8_t *right_rgba, float *cout, float *den, int den_mode, void *stream);
 
+/* ---- support arrays in INDEX form (the support stream of a d-shard) ----
+ * A pass reads its direction's two support arrays, 8*T*S bytes, whatever its plane
+ * count: as many bytes as the cost stream of a 32-plane shard (the C4 frame over 8
+ * GPUs).  In index form, element (y,x,i) is the LUT index dist*766 + SAD of the weight
+ * asw_support writes there (0 in padding taps i >= taps): uint16 [H][W][Tp], half the
+ * bytes, and lut[index] (asw_support_lut) is that weight bit for bit.
+ * asw_support_all_fmt: asw_support_all with a format per array, bit j of index_mask
+ * (j = 0 wvl, 1 whl, 2 wvr, 3 whr) set = that array in index form (a uint16_t *), else
+ * float weights.  Index form needs (R+1)*766 <= 65536 and Tp <= 68 (ASW_E_UNSUPPORTED).
+ * asw_aggregate_pass_index: asw_aggregate_pass_den reading index-form supports and the
+ * LUT, bit-identical to it on the float arrays; built where asw_pass_index_supported
+ * (p, dir, den_mode) says 1 (32-plane shards, RGB, ring tap counts <= 35, the V pass
+ * with ASW_DEN_NONE, which is what such a shard's frame runs); ASW_E_UNSUPPORTED else. */
+size_t asw_support_index_bytes(const asw_params *p); /* H*W*Tp*2 */
+int asw_support_all_fmt(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba, const float *lut,
+                        void *wvl, void *whl, void *wvr, void *whr, int index_mask, void *stream);
+int asw_aggregate_pass_index(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
+                             const float *cin, float *cout, float *den, int den_mode, void *stream);
+int asw_pass_index_supported(const asw_params *p, int dir, int den_mode);
+
 /* r x (V,H) ping-pong of main.cpp:486-515 on two caller buffers; the result
  * ends in `c0` (c0 holds the raw cost on entry, c1 is scratch). */
 int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,

@@ -138,6 +138,10 @@ SIGNATURES = {
     "asw_aggregate_pass_raw": (I, [PP, P, P, P, P, P, P, I, P]),
     "asw_aggregate_pass_otf": (I, [PP, I, P, P, P, P, P, P, I, P]),
     "asw_pass_otf_supported": (I, [PP, I]),
+    "asw_support_index_bytes": (ctypes.c_size_t, [PP]),
+    "asw_support_all_fmt": (I, [PP, P, P, P, P, P, P, P, I, P]),
+    "asw_aggregate_pass_index": (I, [PP, I, P, P, P, P, P, P, I, P]),
+    "asw_pass_index_supported": (I, [PP, I, I]),
     "asw_aggregate": (I, [PP, P, P, P, P, P, P, P]),
     "asw_aggregate_den": (I, [PP, P, P, P, P, P, P, P, P, P]),
     "asw_wta": (I, [PP, P, P, P, P, P, P, P, P]),

@@ -19,6 +19,9 @@ int launch_pass_tm(const asw_params *p, int dir, const float *wl, const float *w
 template <int T, int DM>
 int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                      float *den, hipStream_t st);
+template <int T>
+int launch_pass32_idx_tm(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
+                         const float *cin, float *cout, float *den, int dm, hipStream_t st);
 // a shard of <= 32 planes (pitch 32): the half-wave passes of asw_pass32.h
 template <int T>
 int launch_pass32_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
@@ -103,6 +106,39 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
         default:  // no ring kernel for this T: the generic pass (the fused raw cost is opt-in, ring kernels only)
             if (raw) return ASW_E_UNSUPPORTED;
             return launch_pass_any(p, dir, wl, wr, cin, cout, den, dm, st);
+    }
+}
+
+// the pass over index-form supports (asw_aggregate_pass_index): 32-plane shards, ring
+// tap counts <= 35, V with den mode NONE (what the shard's frame runs), H in every mode
+bool pass_index_supported(const asw_params *p, int dir, int dm) {
+    const int T = p->taps;
+    if (dir == ASW_DIR_V && dm != ASW_DEN_NONE) return false;
+    return (dir == ASW_DIR_V || dir == ASW_DIR_H) && dm >= ASW_DEN_NONE && dm <= ASW_DEN_READ &&
+           p->color_space == ASW_COLOR_RGB && asw_disp_pitch(p) == 32 && ring_taps(T) && T <= 35;
+}
+
+int launch_pass_index(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
+                      const float *cin, float *cout, float *den, int dm, hipStream_t st) {
+    if (const int s = pass_shape_check(p)) return s;
+    if (!pass_index_supported(p, dir, dm)) return ASW_E_UNSUPPORTED;
+#ifdef ASW_DEV_TAPS
+    if (p->taps == ASW_DEV_TAPS) return agg::launch_pass32_idx_tm<ASW_DEV_TAPS>(p, dir, wl, wr, lut, cin, cout, den, dm, st);
+    return ASW_E_UNSUPPORTED;
+#endif
+    switch (p->taps) {
+#define ASW_CASE(TT) \
+    case TT:         \
+        return agg::launch_pass32_idx_tm<TT>(p, dir, wl, wr, lut, cin, cout, den, dm, st);
+        ASW_CASE(3)
+        ASW_CASE(5)
+        ASW_CASE(7)
+        ASW_CASE(9)
+        ASW_CASE(15)
+        ASW_CASE(33)
+        ASW_CASE(35)
+#undef ASW_CASE
+        default: return ASW_E_UNSUPPORTED;
     }
 }
 

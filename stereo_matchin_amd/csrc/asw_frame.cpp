@@ -40,6 +40,8 @@ struct Shard {
     float *c0 = nullptr, *c1 = nullptr;                                    // [H][W][Dp]
     float *den_v = nullptr, *den_h = nullptr;  // cached denominators (iters >= 2)
     bool otf = false;  // the H passes compute the right weights on the fly (whr not allocated)
+    bool vidx = false; // wvl / wvr in index form (uint16 LUT indices; asw_aggregate_pass_index)
+    bool hidx = false; // whl / whr likewise
     // d-sharded WTA (more than one shard in the frame)
     int64_t *key = nullptr, *key_g = nullptr, *tkey = nullptr, *tkey_g = nullptr;
     float *m1 = nullptr, *m2 = nullptr, *t1 = nullptr, *t2 = nullptr, *m2_g = nullptr, *t2_g = nullptr;
@@ -257,15 +259,27 @@ int alloc_shard(Shard &s, bool sharded) {
         ASWCHK(dev_alloc(&s.lab_l, asw_lab_bytes(p)));
         ASWCHK(dev_alloc(&s.lab_r, asw_lab_bytes(p)));
     }
-    ASWCHK(dev_alloc(&s.wvl, asw_support_bytes(p)));
-    ASWCHK(dev_alloc(&s.wvr, asw_support_bytes(p)));
-    ASWCHK(dev_alloc(&s.whl, asw_support_bytes(p)));
+    // a 32-plane shard can read its supports in index form (uint16 LUT
+    // indices, half the bytes of the replicated support stream; asw_aggregate_pass_index),
+    // bit-identical but measured slower: its passes are LDS-bound and the LUT reads cost
+    // more LDS cycles than the bytes save (C4 / 8: V 0.351 against 0.265 ms, H 0.68 against
+    // 0.36; shard frame 7.10 against 5.13 ms, profiles/r04/index_form_r10b.log).  Opt-in:
+    // ASW_SUPPORT_INDEX=1 (both directions) or =v (the V passes only)
+    const char *idx_env = std::getenv("ASW_SUPPORT_INDEX");
+    const bool idx_on = idx_env && (idx_env[0] == '1' || idx_env[0] == 'v'), v_only = idx_env && idx_env[0] == 'v';
+    s.vidx = idx_on && asw_pass_index_supported(p, ASW_DIR_V, ASW_DEN_NONE) != 0;
+    s.hidx = idx_on && !v_only && s.vidx && asw_pass_index_supported(p, ASW_DIR_H, ASW_DEN_READ) != 0;
+    const size_t vbytes = s.vidx ? asw_support_index_bytes(p) : asw_support_bytes(p);
+    const size_t hbytes = s.hidx ? asw_support_index_bytes(p) : asw_support_bytes(p);
+    ASWCHK(dev_alloc(&s.wvl, vbytes));
+    ASWCHK(dev_alloc(&s.wvr, vbytes));
+    ASWCHK(dev_alloc(&s.whl, hbytes));
     // the right H weights can be computed inside the H passes
     // (asw_aggregate_pass_otf, the array then never built): bit-identical but measured
     // slower at C4 (H den-read 2.30 against 1.42 ms), so only on request (ASW_OTF=1)
     const char *otf_env = std::getenv("ASW_OTF");
     s.otf = otf_env && otf_env[0] == '1' && asw_pass_otf_supported(p, ASW_DIR_H) != 0;
-    if (!s.otf) ASWCHK(dev_alloc(&s.whr, asw_support_bytes(p)));
+    if (!s.otf) ASWCHK(dev_alloc(&s.whr, hbytes));
     ASWCHK(dev_alloc(&s.c0, asw_cost_bytes(p)));
     ASWCHK(dev_alloc(&s.c1, asw_cost_bytes(p)));
     if (p->iters >= 2) {  // the den of a direction is written by its first pass and read by the r-1 others
@@ -431,15 +445,24 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         ASWCHK(asw_support_lab(p, ASW_DIR_H, s.lab_r, s.whr, st));
     } else {
         ASWCHK(asw_support_lut(p, s.lut, st));
-        ASWCHK(asw_support_all(p, s.left, s.right, s.lut, s.wvl, s.whl, s.wvr, s.otf ? nullptr : s.whr, st));
+        ASWCHK(asw_support_all_fmt(p, s.left, s.right, s.lut, s.wvl, s.whl, s.wvr, s.otf ? nullptr : s.whr,
+                                   (s.vidx ? 5 : 0) | (s.hidx ? 10 : 0), st));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0], st));
     for (int it = 0; it < p->iters; ++it) {
         const int dmv = !s.den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
         const int dm = !s.den_h ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
-        ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, s.wvl, s.wvr, s.c0, s.c1, s.den_v, dmv, st));
+        if (s.vidx)
+            ASWCHK(asw_aggregate_pass_index(p, ASW_DIR_V, reinterpret_cast<const uint16_t *>(s.wvl),
+                                            reinterpret_cast<const uint16_t *>(s.wvr), s.lut, s.c0, s.c1, nullptr,
+                                            ASW_DEN_NONE, st));
+        else ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, s.wvl, s.wvr, s.c0, s.c1, s.den_v, dmv, st));
         if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0 + 2 * it + 1], st));
         if (s.otf) ASWCHK(asw_aggregate_pass_otf(p, ASW_DIR_H, s.whl, s.right, s.lut, s.c1, s.c0, s.den_h, dm, st));
+        else if (s.hidx)
+            ASWCHK(asw_aggregate_pass_index(p, ASW_DIR_H, reinterpret_cast<const uint16_t *>(s.whl),
+                                            reinterpret_cast<const uint16_t *>(s.whr), s.lut, s.c1, s.c0, s.den_h, dm,
+                                            st));
         else ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, s.whl, s.whr, s.c1, s.c0, s.den_h, dm, st));
         if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0 + 2 * it + 2], st));
     }

@@ -88,7 +88,11 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
                                                    float *__restrict__ cost, int W, int Dp, int nloc, int d_begin,
                                                    float tau) {
     using f4 = float __attribute__((ext_vector_type(4)));
-    extern __shared__ uchar4 rrow[];  // R[y][xr], xr in [xlo, x0 + kRawSpan)
+    // R[y][xr], xr in [xlo, x0 + kRawSpan), element t at t + t/32: the lanes of a read
+    // are 4 elements apart (planes 4q..4q+3), so one pad dword per 32 puts the 32 lanes
+    // of a half-wave on 32 different banks (unpadded: 4-way conflicts)
+    extern __shared__ uchar4 rrow[];
+    auto slot = [](int t) __attribute__((always_inline)) { return t + (t >> 5); };
     const int y = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uchar4 *Lrow = L + (long long)y * W, *Rrow = R + (long long)y * W;
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
     const int nr = kRawSpan + Dp - 1;
     for (int t = threadIdx.x; t < nr; t += 256) {
         const int xr = xlo + t;
-        rrow[t] = Rrow[xr < 0 ? 0 : (xr >= W ? W - 1 : xr)];
+        rrow[slot(t)] = Rrow[xr < 0 ? 0 : (xr >= W ? W - 1 : xr)];
     }
     __syncthreads();
     const int nq = Dp >> 2;
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
             for (int j = 0; j < 4; ++j) {
                 const int k = 4 * q + j;
                 const int d = d_begin + k;
-                const uchar4 r = rrow[x - d - xlo];  // = R(max(x-d, 0), y): the stage clamps
+                const uchar4 r = rrow[slot(x - d - xlo)];  // = R(max(x-d, 0), y): the stage clamps
                 float sv = fabsf((float)l.x - (float)r.x) + fabsf((float)l.y - (float)r.y);
                 sv = sv + fabsf((float)l.z - (float)r.z);
                 v[j] = k < nloc ? fminf(sv, tau) : 0.0f;
@@ -138,8 +142,9 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
 // ---------------------------------------------------------------------------
 struct SupportJobs {
     const uchar4 *img[4];
-    float *w[4];
+    float *w[4];  // (index form: uint16_t [H][W][Tp] behind the pointer)
     int dir[4];
+    int idx[4];   // 1: write the LUT index dist*766 + SAD of each weight (asw_support_all_fmt)
 };
 template <int Q>
 __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *__restrict__ lut, int W, int H,
@@ -168,6 +173,41 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
             const int qx = dir == ASW_DIR_V ? x : clampi(x + k - R, 0, W - 1);
             const int qy = dir == ASW_DIR_V ? clampi(y + k - R, 0, H - 1) : y;
             b[k] = img[qy * W + qx];
+        }
+        if (jobs.idx[blockIdx.z]) {
+            // index form: the weight's LUT index instead of the weight (no gathers),
+            // four uint16 per 8-B share, transposed through LDS like the weights
+            using u2 = unsigned __attribute__((ext_vector_type(2)));
+            u2 c[NG];
+#pragma unroll
+            for (int k = 0; k < 4 * NG; ++k) {
+                int dist;
+                if (dir == ASW_DIR_V) {
+                    const int qy = clampi(y + k - R, 0, H - 1);
+                    dist = y > qy ? y - qy : qy - y;
+                } else {
+                    const int qx = clampi(x + k - R, 0, W - 1);
+                    dist = x > qx ? x - qx : qx - x;
+                }
+                const int sad = abs((int)a.x - (int)b[k].x) + abs((int)a.y - (int)b[k].y) + abs((int)a.z - (int)b[k].z);
+                const unsigned ix = k < T ? (unsigned)(dist * kLutWidth + sad) : 0u;
+                if (k % 2 == 0) c[k / 4][(k % 4) / 2] = ix;
+                else c[k / 4][(k % 4) / 2] |= ix << 16;
+            }
+            u2 *st2 = reinterpret_cast<u2 *>(stg[wv]);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) st2[lane * Q + g] = c[g];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int nval = min(64, W - x0) * Q;
+            u2 *out = reinterpret_cast<u2 *>(jobs.w[blockIdx.z]) + ((long long)y * W + x0) * Q;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const int e = g * 64 + lane;
+                if (e < nval) out[e] = st2[e];
+            }
+            return;
         }
         f4 v[NG];
 #pragma unroll
@@ -577,6 +617,10 @@ using namespace asw;
 // C-ABI: parameters and layout
 // ===========================================================================
 namespace asw {
+// asw_aggregate.hip: the pass over index-form supports
+bool pass_index_supported(const asw_params *p, int dir, int dm);
+int launch_pass_index(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
+                      const float *cin, float *cout, float *den, int dm, hipStream_t st);
 // asw_wta_sweep.hip: asw_WTA as a row sweep (ASW_E_UNSUPPORTED for pitches it is not built for)
 int launch_wta_sweep(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
                      float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, hipStream_t st);
@@ -596,9 +640,9 @@ int asw_tune_set(int key, int value) {
     if (key == ASW_TUNE_PASS_VARIANT) {
         // only bits that select a compiled form (launch_dm): a stale bit would time the
         // default kernel under another name
-        // (+ bits 16-24: strip / segment counts and the lean H form of the 32-plane
-        // shard passes, asw_pass32.h)
-        if (value & ~(asw::kPassVariantBits | 0x1FF0000)) return ASW_E_INVALID;
+        // (+ bits 16-25: strip / segment counts, the lean H form and the index-form H
+        // phases of the 32-plane shard passes, asw_pass32.h)
+        if (value & ~(asw::kPassVariantBits | 0x3FF0000)) return ASW_E_INVALID;
         return asw::set_pass_variant(value);
     }
     if (key == ASW_TUNE_WTA_VARIANT) {
@@ -686,7 +730,7 @@ int asw_raw_cost(const asw_params *p, const uint8_t *left, const uint8_t *right,
     if (!left || !right || !cost) return ASW_E_INVALID;
     const int Dp = asw_disp_pitch(p);
     const dim3 grid((unsigned)((p->width + kRawSpan - 1) / kRawSpan), (unsigned)p->height);
-    const size_t lds = (size_t)(kRawSpan + Dp - 1) * 4;
+    const size_t lds = (size_t)((kRawSpan + Dp - 1) + (kRawSpan + Dp - 1) / 32 + 1) * 4;
     if (lds > 64 * 1024) return ASW_E_UNSUPPORTED;
     hipLaunchKernelGGL(k_raw_cost, grid, dim3(256), lds, (hipStream_t)stream, reinterpret_cast<const uchar4 *>(left),
                        reinterpret_cast<const uchar4 *>(right), cost, p->width, Dp, d_end_of(p) - p->d_begin,
@@ -706,6 +750,10 @@ int asw_support_lut(const asw_params *p, float *lut, void *stream) {
 
 static int launch_support(const asw_params *p, const SupportJobs &jobs, int njobs, const float *lut, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
+    bool any_idx = false;
+    for (int j = 0; j < njobs; ++j) any_idx = any_idx || jobs.idx[j];
+    // index form: uint16 indices of the (R+1) x 766 LUT, the unrolled kernels only
+    if (any_idx && ((p->taps / 2 + 1) * kLutWidth > 65536 || asw_tap_pitch(p) > 68)) return ASW_E_UNSUPPORTED;
     switch (asw_tap_pitch(p) / 4) {  // Tp = 4Q, Q odd past 1 (tap_pitch)
         case 1: launch_support_q<1>(p, jobs, njobs, lut, st); break;
         case 3: launch_support_q<3>(p, jobs, njobs, lut, st); break;
@@ -736,24 +784,34 @@ int asw_support(const asw_params *p, int dir, const uint8_t *img, const float *l
     return launch_support(p, jobs, 1, lut, stream);
 }
 
-int asw_support_all(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut, float *wvl,
-                    float *whl, float *wvr, float *whr, void *stream) {
+int asw_support_all_fmt(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut, void *wvl,
+                        void *whl, void *wvr, void *whr, int index_mask, void *stream) {
     ASW_CHECK_PARAMS(p);
-    if (!left || !right || !lut || !(wvl || whl || wvr || whr)) return ASW_E_INVALID;
+    if (!left || !right || !lut || !(wvl || whl || wvr || whr) || (index_mask & ~15)) return ASW_E_INVALID;
     if (p->color_space != ASW_COLOR_RGB) return ASW_E_INVALID;
     SupportJobs jobs{};
     const uchar4 *img[4] = {reinterpret_cast<const uchar4 *>(left), reinterpret_cast<const uchar4 *>(left),
                             reinterpret_cast<const uchar4 *>(right), reinterpret_cast<const uchar4 *>(right)};
-    float *w[4] = {wvl, whl, wvr, whr};
+    void *w[4] = {wvl, whl, wvr, whr};
     int n = 0;
     for (int j = 0; j < 4; ++j) {
         if (!w[j]) continue;  // an array the caller computes on the fly (asw_aggregate_pass_otf)
         jobs.img[n] = img[j];
-        jobs.w[n] = w[j];
+        jobs.w[n] = static_cast<float *>(w[j]);
         jobs.dir[n] = (j & 1) ? ASW_DIR_H : ASW_DIR_V;
+        jobs.idx[n] = (index_mask >> j) & 1;
         ++n;
     }
     return launch_support(p, jobs, n, lut, stream);
+}
+
+int asw_support_all(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut, float *wvl,
+                    float *whl, float *wvr, float *whr, void *stream) {
+    return asw_support_all_fmt(p, left, right, lut, wvl, whl, wvr, whr, 0, stream);
+}
+
+size_t asw_support_index_bytes(const asw_params *p) {
+    return (size_t)p->width * p->height * (size_t)asw_tap_pitch(p) * sizeof(uint16_t);
 }
 
 int asw_lab(const asw_params *p, const uint8_t *img, float *lab, void *stream) {
@@ -803,6 +861,21 @@ int asw_aggregate_pass_otf(const asw_params *p, int dir, const float *wl, const 
     if (dir != ASW_DIR_H || p->color_space != ASW_COLOR_RGB || !asw::ring_taps(p->taps)) return ASW_E_UNSUPPORTED;
     const asw::OtfSrc otf{right_rgba, lut};
     return asw::launch_pass(p, dir, wl, nullptr, cin, cout, den, den_mode, (hipStream_t)stream, nullptr, &otf);
+}
+
+int asw_aggregate_pass_index(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
+                             const float *cin, float *cout, float *den, int den_mode, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!wl || !wr || !lut || !cin || !cout || cin == cout || (dir != ASW_DIR_V && dir != ASW_DIR_H))
+        return ASW_E_INVALID;
+    if (den_mode < ASW_DEN_NONE || den_mode > ASW_DEN_READ) return ASW_E_INVALID;
+    if (den_mode != ASW_DEN_NONE && (!den || den == cin || den == cout)) return ASW_E_INVALID;
+    return asw::launch_pass_index(p, dir, wl, wr, lut, cin, cout, den, den_mode, (hipStream_t)stream);
+}
+
+int asw_pass_index_supported(const asw_params *p, int dir, int den_mode) {
+    if (!p || asw_params_check(p) != ASW_OK) return 0;
+    return asw::pass_index_supported(p, dir, den_mode) ? 1 : 0;
 }
 
 int asw_pass_otf_supported(const asw_params *p, int dir) {

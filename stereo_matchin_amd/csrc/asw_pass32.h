@@ -19,12 +19,15 @@
 //              x; its right and left entries live in a wave-private LDS ring per row
 //              (no block barrier: the waves of a block share nothing).
 #pragma once
+#include <cstdio>
+
 #include "asw_aggregate_impl.h"
 
 namespace asw {
 namespace agg {
 
 constexpr int kPlanes32 = 32;
+using u2 = unsigned __attribute__((ext_vector_type(2)));  // four uint16 LUT indices
 
 // taps [B, E) of a phase with per-lane left weights (wl, wr hold taps from B)
 template <int U, int S, int B, int E, bool DEN, int M>
@@ -45,10 +48,16 @@ __device__ __forceinline__ void taps32(float &num, float &den, const f4 (&wl)[M]
 // NBUF-deep LDS ring of row slabs written LEAD rows ahead, one barrier per RB rows,
 // weights in NPH phases with two phases' sets live).
 // ---------------------------------------------------------------------------
-template <int T, int NW, int DM, int CP, int NPH, int RB = 2, int PS = 4>
+//
+// IDX: the support arrays are in index form (asw_support_all_fmt: uint16 LUT indices,
+// half the bytes): the block copies the LUT into LDS once and each staged float4 is
+// looked up there (4 ds_read_b32) before it enters the slab ring; the taps then run
+// on the same float weights, so the result is bit-identical.
+template <int T, int NW, int DM, int CP, int NPH, bool IDX = false, int RB = 2, int PS = 4>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 4 : 2))) void k_vpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
-    float *__restrict__ den, int W, int H, int d_begin, int rows_per_strip, int nxb, int nstrip, int xg_per_xcd) {
+    float *__restrict__ den, int W, int H, int d_begin, int rows_per_strip, int nxb, int nstrip, int xg_per_xcd,
+    const float *__restrict__ lut) {
     constexpr int R = T / 2;
     constexpr int TP = tap_pitch(T);
     constexpr int Q = TP / 4;
@@ -67,6 +76,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     constexpr int NSTAGE = (NQ + NW * 64 - 1) / (NW * 64);
     static_assert(NSTAGE <= 2, "slab row larger than two float4 per thread");
     __shared__ f4 slab[NBUF][NQ];
+    constexpr int NLUT = IDX ? (R + 1) * kLutWidth : 1;
+    __shared__ float lut_s[NLUT];
 
     const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
     const int xg = xcd * xg_per_xcd + m % xg_per_xcd;
@@ -96,24 +107,49 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     // x0 + e - NER (both clamped into the row); surplus threads redo the last one
     const int t0 = min((int)threadIdx.x, NQ - 1);
     const int t1 = min((int)threadIdx.x + NW * 64, NQ - 1);
+    // element offset of share t's float4 in its (row 0) support row: right weights of
+    // entries < NER, else left
     auto src_of = [&](int t) __attribute__((always_inline)) {
         const int e = t / Q, q = t - e * Q;
-        if (e < NER) return wr + clampi(x0 - d_begin - 31 + e, 0, W - 1) * TP + 4 * q;
-        return wl + min(x0 + e - NER, W - 1) * TP + 4 * q;
+        if (e < NER) return clampi(x0 - d_begin - 31 + e, 0, W - 1) * TP + 4 * q;
+        return min(x0 + e - NER, W - 1) * TP + 4 * q;
     };
-    const float *src0 = src_of(t0), *src1 = src_of(t1);
-    auto stage = [&](f4 &a, f4 &b, int row) __attribute__((always_inline)) {
-        a = *reinterpret_cast<const f4 *>(src0 + row * wrow);
-        if constexpr (NSTAGE > 1) b = *reinterpret_cast<const f4 *>(src1 + row * wrow);
+    const int o0 = src_of(t0), o1 = src_of(t1);
+    const bool r0 = t0 / Q < NER, r1 = t1 / Q < NER;
+    // staged share: 4 weights (f4) or 4 LUT indices (u2, two uint16 per dword)
+    using stg_t = std::conditional_t<IDX, u2, f4>;
+    using elem_t = std::conditional_t<IDX, uint16_t, float>;
+    const elem_t *src0 = reinterpret_cast<const elem_t *>(r0 ? wr : wl) + o0;
+    const elem_t *src1 = reinterpret_cast<const elem_t *>(r1 ? wr : wl) + o1;
+    auto stage = [&](stg_t &a, stg_t &b, int row) __attribute__((always_inline)) {
+        a = *reinterpret_cast<const stg_t *>(src0 + row * wrow);
+        if constexpr (NSTAGE > 1) b = *reinterpret_cast<const stg_t *>(src1 + row * wrow);
+    };
+    // the float4 of a staged share (IDX: four LUT reads from LDS)
+    auto weights = [&](const stg_t &a) __attribute__((always_inline)) {
+        if constexpr (IDX) {
+            f4 v;
+            v[0] = lut_s[a[0] & 0xFFFFu];
+            v[1] = lut_s[a[0] >> 16];
+            v[2] = lut_s[a[1] & 0xFFFFu];
+            v[3] = lut_s[a[1] >> 16];
+            return v;
+        } else {
+            return a;
+        }
     };
     auto put = [&](int buf, const f4 &a, const f4 &b) __attribute__((always_inline)) {
         slab[buf][t0] = a;
         if constexpr (NSTAGE > 1) slab[buf][t1] = b;
     };
+    if constexpr (IDX) {
+        for (int t = threadIdx.x; t < NLUT; t += NW * 64) lut_s[t] = lut[t];
+        __syncthreads();
+    }
 
     using PH = Phases<T, NPH>;
     float win[U];
-    f4 sa[PS], sb[PS];
+    stg_t sa[PS], sb[PS];
     f4 wlp[NPH][PH::NG], wrp[NPH][PH::NG];
     float dring[KD];
     {
@@ -130,7 +166,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
 #pragma unroll
     for (int j = 0; j < PS; ++j) stage(sa[j], sb[j], min(y_begin + j, H - 1));
 #pragma unroll
-    for (int j = 0; j < LEAD; ++j) put(j, sa[j], sb[j]);
+    for (int j = 0; j < LEAD; ++j) put(j, weights(sa[j]), weights(sb[j]));
 #pragma unroll
     for (int j = 0; j < LEAD; ++j) stage(sa[j], sb[j], min(y_begin + PS + j, H - 1));
     __syncthreads();
@@ -139,6 +175,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
         read_wr<T, PH::gb(k), PH::gb(k + 1)>(wlp[k], &slab[buf][my_wl]);
         read_wr<T, PH::gb(k), PH::gb(k + 1)>(wrp[k], &slab[buf][my_wr]);
     };
+    (void)r1;
     request(std::integral_constant<int, 0>{}, 0);
 
     auto chunk = [&](auto clamp_c, int ys) __attribute__((always_inline)) {
@@ -165,10 +202,17 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
                 else wait_lgkm0();
                 if constexpr (k == 0) asm volatile("" ::"v"(win[(s + T - 1) % U]));  // one vmcnt wait per step
                 __builtin_amdgcn_sched_barrier(0);
+                // (IDX: the staged row's LUT reads go out before the weight requests, so
+                // the slab write waits for them alone)
+                f4 pa, pb;
+                if constexpr (k == 0) {
+                    pa = weights(sa[(s + LEAD) % PS]);
+                    if constexpr (NSTAGE > 1) pb = weights(sb[(s + LEAD) % PS]);
+                }
                 if constexpr (k + 1 < NPH) request(std::integral_constant<int, k + 1>{}, bcur);
                 else request(std::integral_constant<int, 0>{}, bnext);
                 if constexpr (k == 0) {
-                    put(bput, sa[(s + LEAD) % PS], sb[(s + LEAD) % PS]);
+                    put(bput, pa, pb);
                     stage(sa[(s + LEAD) % PS], sb[(s + LEAD) % PS], min(y + LEAD + PS, H - 1));
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -211,17 +255,21 @@ constexpr int h32_batch(int T) { return tap_pitch(T) / 4 * 8 <= 64 * 4 ? 4 : 2; 
 
 // RING16: right ring of a multiple of 16 entries (conflict-free across the wrap) or
 // the minimal 32 + 2K (a 2-way conflict where a read wraps; less LDS, more waves)
-template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2>
+// IDX: index-form supports (uint16 LUT indices): the block's waves share one LDS copy
+// of the LUT, and each staged float4 is looked up there before it enters the ring.
+// KB: the refill batch (0: h32_batch).
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0>
 __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_hpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
-    float *__restrict__ den, int W, int H, int d_begin, int nseg, int seg_len, int npairs, int pairs_per_xcd) {
+    float *__restrict__ den, int W, int H, int d_begin, int nseg, int seg_len, int npairs, int pairs_per_xcd,
+    const float *__restrict__ lut) {
     constexpr int R = T / 2;
     constexpr int TP = tap_pitch(T);
     constexpr int Q = TP / 4;
     constexpr int U = pf9_period(T);
     constexpr int P = U - T;
     constexpr int KD = 4;  // den prefetch ring (steps)
-    constexpr int K = h32_batch(T);
+    constexpr int K = KB ? KB : h32_batch(T);
     constexpr int RING = RING16 ? (32 + 2 * K + 15) / 16 * 16 : 32 + 2 * K;  // right entries per row
     constexpr int LRING = 2 * K + 2;                   // left entries per row
     constexpr int ROWE = RING + LRING;                 // ring entries per row
@@ -230,6 +278,12 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     constexpr int NST = 4 * K * Q;
     constexpr int SPL = (NST + 63) / 64;  // float4 per lane
     __shared__ f4 ring_all[NWB][2 * ROWE * Q];
+    constexpr int NLUT = IDX ? (R + 1) * kLutWidth : 1;
+    __shared__ float lut_s[NLUT];
+    if constexpr (IDX) {  // (before any wave leaves: the one block barrier)
+        for (int t = threadIdx.x; t < NLUT; t += NWB * 64) lut_s[t] = lut[t];
+        __syncthreads();
+    }
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -252,9 +306,24 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     // n = ((r*2 + kind)*K + k)*Q + q: row r, kind 0 = right entry xb+1-d0+k, kind 1 =
     // left entry xb+1+k of the batch whose first step is xb (its entries are written at
     // the top of batch xb - K, the batch before the one that first reads them)
-    const float *wrrows[2] = {wr + (long long)min(2 * pr, H - 1) * W * TP, wr + (long long)min(2 * pr + 1, H - 1) * W * TP};
-    const float *wlrows[2] = {wl + (long long)min(2 * pr, H - 1) * W * TP, wl + (long long)min(2 * pr + 1, H - 1) * W * TP};
-    const float *st_row[SPL];
+    using stg_t = std::conditional_t<IDX, u2, f4>;  // a staged share: 4 weights or 4 LUT indices
+    using elem_t = std::conditional_t<IDX, uint16_t, float>;
+    const elem_t *wre = reinterpret_cast<const elem_t *>(wr), *wle = reinterpret_cast<const elem_t *>(wl);
+    const elem_t *wrrows[2] = {wre + (long long)min(2 * pr, H - 1) * W * TP, wre + (long long)min(2 * pr + 1, H - 1) * W * TP};
+    const elem_t *wlrows[2] = {wle + (long long)min(2 * pr, H - 1) * W * TP, wle + (long long)min(2 * pr + 1, H - 1) * W * TP};
+    auto weights = [&](const stg_t &a) __attribute__((always_inline)) {
+        if constexpr (IDX) {
+            f4 v;
+            v[0] = lut_s[a[0] & 0xFFFFu];
+            v[1] = lut_s[a[0] >> 16];
+            v[2] = lut_s[a[1] & 0xFFFFu];
+            v[3] = lut_s[a[1] >> 16];
+            return v;
+        } else {
+            return a;
+        }
+    };
+    const elem_t *st_row[SPL];
     int st_q4[SPL], st_k[SPL], st_kind[SPL], st_slot[SPL], st_base[SPL];
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
@@ -273,7 +342,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     auto st_load = [&](int j, int xb) __attribute__((always_inline)) {  // entry of the batch starting at xb
         const int e = xb + 1 + st_k[j];
         const int c = st_kind[j] == 0 ? clampi(e - d0, 0, W - 1) : min(e, W - 1);
-        return *reinterpret_cast<const f4 *>(st_row[j] + c * TP + st_q4[j]);
+        return *reinterpret_cast<const stg_t *>(st_row[j] + c * TP + st_q4[j]);
     };
 
     // the rings before step xs: right entries [xs-d0-31, xs+K-d0], left [xs, xs+K]
@@ -285,16 +354,16 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
         int slot;
         if (e < NR0) {
             const int xr = xs - d0 - 31 + e;
-            v = *reinterpret_cast<const f4 *>(wrrows[r] + clampi(xr, 0, W - 1) * TP + 4 * q);
+            v = weights(*reinterpret_cast<const stg_t *>(wrrows[r] + clampi(xr, 0, W - 1) * TP + 4 * q));
             slot = (xr + (1 << 20)) % RING;
         } else {
             const int x = xs + e - NR0;
-            v = *reinterpret_cast<const f4 *>(wlrows[r] + min(x, W - 1) * TP + 4 * q);
+            v = weights(*reinterpret_cast<const stg_t *>(wlrows[r] + min(x, W - 1) * TP + 4 * q));
             slot = RING + x % LRING;
         }
         ring[(r * ROWE + slot) * Q + q] = v;
     }
-    f4 stg[SPL];
+    stg_t stg[SPL];
 #pragma unroll
     for (int j = 0; j < SPL; ++j) stg[j] = st_load(j, xs + K);
 
@@ -339,9 +408,12 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
         if constexpr (s % K == 0) {
             // top of a batch (steps [x, x+K)): write the entries the next batch reads
             // first (loaded a batch ago), then load the ones after them
+            f4 wv[SPL];  // (IDX: every share's LUT reads before the first ring write)
+#pragma unroll
+            for (int j = 0; j < SPL; ++j) wv[j] = weights(stg[j]);
 #pragma unroll
             for (int j = 0; j < SPL; ++j) {
-                ring[st_slot[j]] = stg[j];
+                ring[st_slot[j]] = wv[j];
                 // advance the slot by K entries inside its ring (RING or LRING entries)
                 const int lim = st_kind[j] == 0 ? RING * Q : LRING * Q;
                 int rel = st_slot[j] - st_base[j] + K * Q;
@@ -382,9 +454,9 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 // ---------------------------------------------------------------------------
 // launchers (one (T, DM) per translation unit: build/p32_t<T>_d<DM>.hip)
 // ---------------------------------------------------------------------------
-template <int T, int NW, int DM, int CP, int NPH>
+template <int T, int NW, int DM, int CP, int NPH, bool IDX = false>
 void launch_v32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
-                hipStream_t st) {
+                hipStream_t st, const float *lut = nullptr) {
     constexpr int U = pf9_period(T);
     const int W = p->width, H = p->height;
     const int nxb = (W + 2 * NW - 1) / (2 * NW);
@@ -401,24 +473,28 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
     const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
     nstrip = (H + rows - 1) / rows;
     const int per_xcd = (nxb + 7) / 8;
-    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl, wr, cin,
-                       cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd);
-    note_pass_kernel(ASW_DIR_V, DM, "k_vpass32", T, NW == 16 ? (NPH == 4 ? "NW=16,NPH=4" : "NW=16") : "NW=8,NPH=3",
+    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, IDX>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl, wr,
+                       cin, cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd, lut);
+    note_pass_kernel(ASW_DIR_V, DM, "k_vpass32", T,
+                     NW == 16 ? (NPH == 4 ? (IDX ? "NW=16,NPH=4,IDX" : "NW=16,NPH=4") : (IDX ? "NW=16,IDX" : "NW=16"))
+                              : "NW=8,NPH=3",
                      CP == kCPStream);
 }
 
-template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2>
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0>
 void launch_h32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
-                hipStream_t st, int seg_len) {
+                hipStream_t st, int seg_len, const float *lut = nullptr) {
     const int W = p->width, H = p->height;
     const int nseg = (W + seg_len - 1) / seg_len;
     const int npairs = (H + 1) / 2 * nseg;  // work items: (row pair, segment)
     const int per_xcd = (npairs + 7) / 8;
     const int blocks_per_xcd = (per_xcd + NWB - 1) / NWB;
-    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE>), dim3(8 * blocks_per_xcd), dim3(NWB * 64), 0, st,
-                       wl, wr, cin, cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd);
+    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE, IDX, KB>), dim3(8 * blocks_per_xcd), dim3(NWB * 64),
+                       0, st, wl, wr, cin, cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd, lut);
+    char shape[48];
+    std::snprintf(shape, sizeof shape, "NWB=%d,NPH=%d%s", NWB, NPH, IDX ? ",IDX" : "");
     note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T,
-                     NPH == 4 ? "NWB=1,NPH=4" : NWB == 4 ? "NWB=4" : "NWB=2", CP == kCPStream);
+                     IDX ? shape : NPH == 4 ? "NWB=1,NPH=4" : NWB == 4 ? "NWB=4" : "NWB=2", CP == kCPStream);
 }
 
 inline int finish32() {
@@ -476,8 +552,64 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
     return finish32();
 }
 
+// the V pass over index-form supports (asw_aggregate_pass_index): 16-wave blocks
+// (T <= 35; their slab ring and the (R+1) x 766 LUT fit the 160 KB LDS), den mode
+// NONE (what a 32-plane shard's V passes run)
+// H over index-form supports: blocks of 8 waves share one LDS copy of the LUT (55 KB
+// at T = 35) beside their 8 private rings of the minimal length at refill batches of 2
+// steps (8 x 12 KB): 8 waves per CU, against up to 11 one-wave blocks of the float form.
+template <int T, int DM, int CP>
+void launch_h32_idx(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
+                    hipStream_t st, const float *lut) {
+    constexpr int U = pf9_period(T);
+    const int pairs = (p->height + 1) / 2;
+    int nseg = (2048 + pairs / 2) / (pairs > 0 ? pairs : 1);
+    if ((g_pass_variant >> 20) & 15) nseg = (g_pass_variant >> 20) & 15;
+    if (nseg < 1) nseg = 1;
+    int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
+    if (seg < 2 * U) seg = 2 * U;
+    constexpr int NPH = T >= 33 ? 4 : 2;
+    if (g_pass_variant & (1 << 25))  // (variant bit 25: two weight phases, more registers)
+        launch_h32<T, 8, DM, CP, 2, false, 2, true, 2>(p, wl, wr, cin, cout, den, st, seg, lut);
+    else launch_h32<T, 8, DM, CP, NPH, false, 2, true, 2>(p, wl, wr, cin, cout, den, st, seg, lut);
+}
+
+template <int T>
+int launch_pass32_idx_tm(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
+                         const float *cin, float *cout, float *den, int dm, hipStream_t st) {
+    if constexpr (T > 35) {
+        return ASW_E_UNSUPPORTED;
+    } else {
+        constexpr int NPH = T >= 33 ? 4 : 2;
+        const bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
+        const float *l = reinterpret_cast<const float *>(wl), *r = reinterpret_cast<const float *>(wr);
+        if (dir == ASW_DIR_V) {
+            if (dm != ASW_DEN_NONE) return ASW_E_UNSUPPORTED;
+            if (stream) launch_v32<T, 16, DM_NONE, kCPStream, NPH, true>(p, l, r, cin, cout, nullptr, st, lut);
+            else launch_v32<T, 16, DM_NONE, 0, NPH, true>(p, l, r, cin, cout, nullptr, st, lut);
+        } else {
+            // (every den mode in this one translation unit: the Makefile instantiates the
+            // index passes once per tap count)
+            if (stream) {
+                if (dm == ASW_DEN_READ) launch_h32_idx<T, DM_READ, kCPStream>(p, l, r, cin, cout, den, st, lut);
+                else if (dm == ASW_DEN_WRITE) launch_h32_idx<T, DM_WRITE, kCPStream>(p, l, r, cin, cout, den, st, lut);
+                else launch_h32_idx<T, DM_NONE, kCPStream>(p, l, r, cin, cout, den, st, lut);
+            } else {
+                if (dm == ASW_DEN_READ) launch_h32_idx<T, DM_READ, 0>(p, l, r, cin, cout, den, st, lut);
+                else if (dm == ASW_DEN_WRITE) launch_h32_idx<T, DM_WRITE, 0>(p, l, r, cin, cout, den, st, lut);
+                else launch_h32_idx<T, DM_NONE, 0>(p, l, r, cin, cout, den, st, lut);
+            }
+        }
+        return finish32();
+    }
+}
+
 }  // namespace agg
 }  // namespace asw
+
+#define ASW_INSTANTIATE_PASS32_IDX(TT)                                                                            \
+    template int asw::agg::launch_pass32_idx_tm<TT>(const asw_params *, int, const uint16_t *, const uint16_t *, \
+                                                    const float *, const float *, float *, float *, int, hipStream_t);
 
 #define ASW_INSTANTIATE_PASS32(TT, DM)                                                                            \
     template int asw::agg::launch_pass32_tm<TT, DM>(const asw_params *, int, const float *, const float *,       \

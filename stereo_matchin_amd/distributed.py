@@ -105,12 +105,13 @@ class HipShardOps:
 class ShardedStereoMatcher:
     """One rank's share of a d-sharded frame."""
 
-    def __init__(self, params: AswParams, rank: int, world: int, device="cuda", group=None):
+    def __init__(self, params: AswParams, rank: int, world: int, device="cuda", group=None,
+                 support_index: bool | None = None):
         p = params.copy()
         p.d_begin, p.d_end = shard_range(params.ndisp, rank, world)
         self.p = p
         self.rank, self.world = rank, world
-        self.matcher = StereoMatcher(p, device)
+        self.matcher = StereoMatcher(p, device, support_index=support_index)
         self.ops = HipShardOps(p)
         self.reduce_min = _allreduce_min_factory(group)
 

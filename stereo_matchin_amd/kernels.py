@@ -105,16 +105,59 @@ def _support(p: AswParams, direction: int, img: torch.Tensor, lut: torch.Tensor 
     return out
 
 
+def new_support_index(p: AswParams, device) -> torch.Tensor:
+    """A support array in index form: uint16 LUT indices [H][W][Tp] (torch has no
+    uint16 arithmetic on every build: int16 storage of the same bits)."""
+    return torch.empty(support_shape(p), dtype=torch.int16, device=device)
+
+
 def support_all(p: AswParams, left: torch.Tensor, right: torch.Tensor, lut: torch.Tensor, wvl: torch.Tensor,
                 whl: torch.Tensor, wvr: torch.Tensor, whr: torch.Tensor) -> None:
-    """asw_vSupport + asw_hSupport of both images in one launch (``asw_support_all``)."""
+    """asw_vSupport + asw_hSupport of both images in one launch (``asw_support_all``).
+
+    An int16 tensor (``new_support_index``) receives that array in index form
+    (``asw_support_all_fmt``): the LUT index of each weight, lut[index] = the weight."""
     for img in (left, right):
         _expect(img, (p.height, p.width, 4), torch.uint8, "image")
-    for w in (wvl, whl, wvr, whr):
-        if w is not None:  # None: not computed (e.g. whr with the on-the-fly H pass)
+    mask = 0
+    for j, w in enumerate((wvl, whl, wvr, whr)):
+        if w is None:  # not computed (e.g. whr with the on-the-fly H pass)
+            continue
+        if w.dtype == torch.int16:
+            mask |= 1 << j
+            _expect(w, support_shape(p), torch.int16, "out")
+        else:
             _expect(w, support_shape(p), torch.float32, "out")
-    _lib.check(_lib.lib().asw_support_all(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(lut), _ptr(wvl), _ptr(whl),
-                                          _ptr(wvr), _ptr(whr), _stream(left.device)), "asw_support_all")
+    _lib.check(_lib.lib().asw_support_all_fmt(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(lut), _ptr(wvl),
+                                              _ptr(whl), _ptr(wvr), _ptr(whr), mask, _stream(left.device)),
+               "asw_support_all_fmt")
+
+
+def index_supported(p: AswParams, direction: int = DIR_V, den_mode: int = 0) -> bool:
+    """asw_pass_index_supported: a pass of (direction, den_mode) reads index-form supports."""
+    return bool(_lib.lib().asw_pass_index_supported(ctypes.byref(p), direction, den_mode))
+
+
+def aggregate_pass_index(p: AswParams, direction: int, supp_left, supp_right, lut, cost_in, out=None, den=None,
+                         den_mode: int = 0):
+    """One aggregation pass over index-form supports (asw_aggregate_pass_index):
+    bit-identical to the pass over the float arrays (lut[index] = the weight)."""
+    _expect(supp_left, support_shape(p), torch.int16, "supp_left")
+    _expect(supp_right, support_shape(p), torch.int16, "supp_right")
+    _expect(lut, lut_shape(p), torch.float32, "lut")
+    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
+    if out is None:
+        out = torch.empty_like(cost_in)
+    _expect(out, cost_shape(p), torch.float32, "out")
+    if out.data_ptr() == cost_in.data_ptr():
+        raise ValueError("aggregation passes are out of place (cost_in != out)")
+    if den_mode:
+        _expect(den, cost_shape(p), torch.float32, "den")
+    _lib.check(_lib.lib().asw_aggregate_pass_index(ctypes.byref(p), direction, _ptr(supp_left), _ptr(supp_right),
+                                                   _ptr(lut), _ptr(cost_in), _ptr(out), _ptr(den), den_mode,
+                                                   _stream(cost_in.device)),
+               "asw_aggregate_pass_index")
+    return out
 
 
 def lab_image(p: AswParams, img: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -49,7 +49,7 @@ class StereoMatcher:
     other r-1 (ASW_DEN_*); bit-identical results, 2 more cost-sized buffers."""
 
     def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool = False,
-                 otf: bool | None = None):
+                 otf: bool | None = None, support_index: bool | str | None = None):
         st = _lib.params_check(params)
         if st != _lib.ASW_OK:
             raise _lib.AswError(st, "asw_params_check")
@@ -69,10 +69,21 @@ class StereoMatcher:
         # raw_and_support returns; the caller's buffer may be reused by then)
         self.right = torch.empty((self.p.height, self.p.width, 4), dtype=torch.uint8, device=dev) \
             if self.otf else None
-        self.wvl = K.new_support(self.p, dev)
-        self.wvr = K.new_support(self.p, dev)
-        self.whl = K.new_support(self.p, dev)
-        self.whr = None if self.otf else K.new_support(self.p, dev)
+        # support_index (opt-in, where built: a 32-plane shard's passes): the supports in
+        # index form, uint16 LUT indices (asw_support_all_fmt), half the bytes of the
+        # replicated support stream; asw_aggregate_pass_index reads them.  "v": the V
+        # passes only.  Bit-identical, measured slower (C4 / 8: V 0.351 against 0.265 ms,
+        # H 0.68 against 0.36; the passes are LDS-bound and the LUT reads cost more LDS
+        # cycles than the halved bytes save; DESIGN.md §Support stream)
+        want = False if support_index is None else support_index
+        self.vidx = bool(want) and K.index_supported(self.p, DIR_V, _lib.DEN_NONE)
+        self.hidx = self.vidx and want != "v" and not self.otf and K.index_supported(self.p, DIR_H, _lib.DEN_READ)
+        new_v = K.new_support_index if self.vidx else K.new_support
+        new_h = K.new_support_index if self.hidx else K.new_support
+        self.wvl = new_v(self.p, dev)
+        self.wvr = new_v(self.p, dev)
+        self.whl = new_h(self.p, dev)
+        self.whr = None if self.otf else new_h(self.p, dev)
         self.c0 = K.new_cost(self.p, dev)
         self.c1 = K.new_cost(self.p, dev)
         self.den_v = self.den_h = None
@@ -115,6 +126,8 @@ class StereoMatcher:
             if it == 0 and images is not None:
                 K.asw_vCostAggregation_raw(p, self.wvl, self.wvr, images[0], images[1], out=self.c1, den=self.den_v,
                                            den_mode=dmv)
+            elif self.vidx:
+                K.aggregate_pass_index(p, DIR_V, self.wvl, self.wvr, self.lut, self.c0, out=self.c1)
             else:
                 K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1, den=self.den_v, den_mode=dmv)
             if events is not None:
@@ -122,6 +135,9 @@ class StereoMatcher:
             if self.otf:
                 K.asw_hCostAggregation_otf(p, self.whl, self.right, self.lut, self.c1, out=self.c0, den=self.den_h,
                                            den_mode=dm)
+            elif self.hidx:
+                K.aggregate_pass_index(p, DIR_H, self.whl, self.whr, self.lut, self.c1, out=self.c0, den=self.den_h,
+                                       den_mode=dm)
             else:
                 K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0, den=self.den_h, den_mode=dm)
             if events is not None:

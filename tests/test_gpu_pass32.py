@@ -110,15 +110,122 @@ def test_c4_shard_band_r7(gpu, oracle):
     d0, d1 = 96, 128  # rank 3 of 8
     Lb, Rb = np.ascontiguousarray(Lh[:band]), np.ascontiguousarray(Rh[:band])
     p = _params(W, band, D, T, iters=r, d_begin=d0, d_end=d1)
-    m = StereoMatcher(p, gpu)
-    m.raw_and_support(_t(Lb, gpu), _t(Rb, gpu))
-    got = plane_major(_np(m.aggregate()), d1 - d0)
-    # (a 32-plane shard recomputes the V denominators, caches the H ones)
-    assert K.pass_kernel(0, 0).startswith("k_vpass32<T=35") and K.pass_kernel(1, 2).startswith("k_hpass32<T=35")
     cost = oracle.raw_cost(Lb, Rb, D)[d0:d1]
     sv = (oracle.support(Lb, T, 0), oracle.support(Rb, T, 0))
     sh = (oracle.support(Lb, T, 1), oracle.support(Rb, T, 1))
     for _ in range(r):
         cost = oracle.aggregate_pass(*sv, cost, T, 0, d0=d0, d1=d1, plane_base=d0)
         cost = oracle.aggregate_pass(*sh, cost, T, 1, d0=d0, d1=d1, plane_base=d0)
-    assert np.array_equal(got, cost), np.argwhere(got != cost)[:5]
+    # float supports (the default), then index-form supports (opt-in)
+    for index in (None, True):
+        m = StereoMatcher(p, gpu, support_index=index)
+        m.raw_and_support(_t(Lb, gpu), _t(Rb, gpu))
+        got = plane_major(_np(m.aggregate()), d1 - d0)
+        # (a 32-plane shard recomputes the V denominators, caches the H ones)
+        tag = ",IDX" if index else ""
+        assert m.vidx == m.hidx == bool(index)
+        assert K.pass_kernel(0, 0).startswith("k_vpass32<T=35,NW=16,NPH=4" + tag), K.pass_kernel(0, 0)
+        assert K.pass_kernel(1, 2).startswith("k_hpass32<T=35,NWB=" + ("8,NPH=4,IDX" if index else "1,NPH=4"))
+        assert np.array_equal(got, cost), (index, np.argwhere(got != cost)[:5])
+        del m
+
+
+# ---------------------------------------------------------------------------
+# index-form supports (asw_support_all_fmt / asw_aggregate_pass_index):
+# uint16 LUT indices in place of the float weights of a 32-plane shard's V passes
+
+
+@pytest.mark.parametrize("T", [3, 9, 35, 51])
+@pytest.mark.parametrize("H,W", [(37, 91), (8, 20), (70, 150)])
+def test_support_index_form_is_lut_index(gpu, T, H, W):
+    """lut[index] equals the float weight asw_support writes, bit for bit, in all four
+    arrays (clamped edges included: the index carries the clamped distance); padding
+    taps hold index 0."""
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    Lh, Rh = _rand_pair(T + H + W, H, W)
+    p = _params(W, H, 256, T)
+    L, R = _t(Lh, gpu), _t(Rh, gpu)
+    lut = K.support_lut(p, gpu)
+    wf = [K.new_support(p, gpu) for _ in range(4)]
+    wi = [K.new_support_index(p, gpu) for _ in range(4)]
+    K.support_all(p, L, R, lut, *wf)
+    K.support_all(p, L, R, lut, *wi)
+    # mixed formats in one launch (what a 32-plane shard computes: V index, H float)
+    wm = [wi[0].clone().zero_(), K.new_support(p, gpu), wi[2].clone().zero_(), K.new_support(p, gpu)]
+    K.support_all(p, L, R, lut, *wm)
+    flat = lut.reshape(-1)
+    for j in range(4):
+        idx = wi[j].to(torch.int32) & 0xFFFF
+        assert int(idx.max()) < flat.numel()
+        got = flat[idx.reshape(-1).long()].reshape(wf[j].shape)
+        got[..., T:] = 0.0
+        assert torch.equal(got.view(torch.int32), wf[j].view(torch.int32)), j
+        assert int(idx[..., T:].abs().sum()) == 0
+    assert torch.equal(wm[0], wi[0]) and torch.equal(wm[2], wi[2])
+    assert torch.equal(wm[1], wf[1]) and torch.equal(wm[3], wf[3])
+
+
+@pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35])
+@pytest.mark.parametrize("H,W,D,d0,d1", [(37, 91, 70, 38, 70), (23, 150, 200, 70, 87), (8, 20, 64, 0, 32),
+                                          (9, 331, 256, 224, 256)])
+@pytest.mark.parametrize("direction", [0, 1])
+def test_pass32_index_bit_exact(gpu, oracle, T, direction, H, W, D, d0, d1):
+    """The passes over index-form supports equal the oracle's pass (and so the float
+    form) bit for bit: V in den mode NONE, H in all three."""
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    Lh, Rh = _rand_pair(T * 7 + W + direction, H, W, shift=6)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
+    Dp = K.cost_shape(p)[2]
+    assert Dp == 32 and K.index_supported(p, direction, 0)
+    L, R = _t(Lh, gpu), _t(Rh, gpu)
+    lut = K.support_lut(p, gpu)
+    iw = [K.new_support_index(p, gpu) for _ in range(4)]
+    K.support_all(p, L, R, lut, *iw)
+    il, ir = (iw[0], iw[2]) if direction == 0 else (iw[1], iw[3])
+    sl, sr = oracle.support(Lh, T, direction), oracle.support(Rh, T, direction)
+    rng = np.random.default_rng(T + D + H)
+    den = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+    modes = (_lib.DEN_NONE,) if direction == 0 else (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ)
+    for mode in modes:
+        cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+        want = oracle.aggregate_pass(sl, sr, cin, T, direction, d0=d0, d1=d1, plane_base=d0)
+        out = K.aggregate_pass_index(p, direction, il, ir, lut, _t(pixel_major(cin, Dp), gpu), den=den,
+                                     den_mode=mode)
+        got = plane_major(_np(out), d1 - d0)
+        assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
+        name = K.pass_kernel(direction, mode)
+        assert name.startswith(("k_vpass32<" if direction == 0 else "k_hpass32<") + f"T={T},") and ",IDX" in name
+
+
+def test_pass_index_supported_shapes(gpu):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    shard = dict(d_begin=224, d_end=256)
+    assert K.index_supported(_params(64, 16, 256, 35, **shard), 0, 0)
+    assert all(K.index_supported(_params(64, 16, 256, 35, **shard), 1, dm) for dm in (0, 1, 2))
+    assert not K.index_supported(_params(64, 16, 256, 35, **shard), 0, 2)       # V: den mode NONE only
+    assert not K.index_supported(_params(64, 16, 256, 51, **shard), 0, 0)       # LUT + slab exceed the LDS
+    assert not K.index_supported(_params(64, 16, 256, 11, **shard), 0, 0)       # no ring kernel
+    assert not K.index_supported(_params(64, 16, 256, 35), 0, 0)                # pitch 64
+    assert not K.index_supported(_params(64, 16, 256, 35, color_space=1, **shard), 0, 0)
+    p = _params(64, 16, 256, 35)
+    x = torch.zeros(K.cost_shape(p), dtype=torch.float32, device=gpu)
+    w = torch.zeros(K.support_shape(p), dtype=torch.int16, device=gpu)
+    lut = K.support_lut(p, gpu)
+    with pytest.raises(_lib.AswError) as e:
+        K.aggregate_pass_index(p, 0, w, w, lut, x, out=x.clone())
+    assert e.value.status == _lib.ASW_E_UNSUPPORTED
+    # a StereoMatcher on a full range keeps float supports; on a shard: on request
+    from stereo_matchin_amd.pipeline import StereoMatcher
+    assert not StereoMatcher(p, gpu, support_index=True).vidx
+    assert StereoMatcher(_params(64, 16, 256, 35, **shard), gpu, support_index=True).vidx
+    assert not StereoMatcher(_params(64, 16, 256, 35, **shard), gpu).vidx
+    m = StereoMatcher(_params(64, 16, 256, 35, **shard), gpu, support_index="v")
+    assert m.vidx and not m.hidx
