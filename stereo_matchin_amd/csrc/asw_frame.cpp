@@ -42,6 +42,7 @@ struct Shard {
     bool otf = false;  // the H passes compute the right weights on the fly (whr not allocated)
     bool vidx = false; // wvl / wvr in index form (uint16 LUT indices; asw_aggregate_pass_index)
     bool hidx = false; // whl / whr likewise
+    bool fuse = false; // asw_Aggr fused into the first V pass (asw_aggregate_pass_raw)
     // d-sharded WTA (more than one shard in the frame)
     int64_t *key = nullptr, *key_g = nullptr, *tkey = nullptr, *tkey_g = nullptr;
     float *m1 = nullptr, *m2 = nullptr, *t1 = nullptr, *t2 = nullptr, *m2_g = nullptr, *t2_g = nullptr;
@@ -259,6 +260,12 @@ int alloc_shard(Shard &s, bool sharded) {
         ASWCHK(dev_alloc(&s.lab_l, asw_lab_bytes(p)));
         ASWCHK(dev_alloc(&s.lab_r, asw_lab_bytes(p)));
     }
+    // asw_Aggr fused into the first V pass (k_vpass10_raw): the raw-cost volume is never
+    // written nor read, bit-identical, but measured slower at C4 (2.40 ms against 0.37 +
+    // 1.78 ms; frame 23.40 either way, profiles/r04/fused_raw_r10d.log), so the two
+    // kernels stay the default; ASW_FUSE_RAW=1 selects the fused pass
+    const char *fuse_env = std::getenv("ASW_FUSE_RAW");
+    s.fuse = fuse_env && fuse_env[0] == '1' && p->iters >= 1 && asw::ring_taps(p->taps) && asw_disp_pitch(p) != 32;
     // a 32-plane shard can read its supports in index form (uint16 LUT
     // indices, half the bytes of the replicated support stream; asw_aggregate_pass_index),
     // bit-identical but measured slower: its passes are LDS-bound and the LUT reads cost
@@ -431,10 +438,8 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         HIPCHK(hipMemcpyAsync(s.right, right_rgba, S * 4, hipMemcpyHostToDevice, st));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_raw], st));
-    // the raw cost volume and the first V pass as two kernels: fusing asw_Aggr into
-    // that pass (asw_aggregate_pass_raw) is bit-identical but measured slower on
-    // MI355X (3.10 ms vs 0.64 + 2.02 ms at C4, profiles/r01/kernel_stats_fused_raw.csv)
-    ASWCHK(asw_raw_cost(p, s.left, s.right, s.c0, st));
+    // the raw cost: its own kernel, or (s.fuse) computed inside the first V pass
+    if (!s.fuse) ASWCHK(asw_raw_cost(p, s.left, s.right, s.c0, st));
     if (timed) HIPCHK(hipEventRecord(c->ev[e_raw + 1], st));
     if (p->color_space == ASW_COLOR_LAB) {
         ASWCHK(asw_lab(p, s.left, s.lab_l, st));
@@ -452,7 +457,9 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
     for (int it = 0; it < p->iters; ++it) {
         const int dmv = !s.den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
         const int dm = !s.den_h ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
-        if (s.vidx)
+        if (it == 0 && s.fuse)
+            ASWCHK(asw_aggregate_pass_raw(p, s.wvl, s.wvr, s.left, s.right, s.c1, s.den_v, dmv, st));
+        else if (s.vidx)
             ASWCHK(asw_aggregate_pass_index(p, ASW_DIR_V, reinterpret_cast<const uint16_t *>(s.wvl),
                                             reinterpret_cast<const uint16_t *>(s.wvr), s.lut, s.c0, s.c1, nullptr,
                                             ASW_DEN_NONE, st));

@@ -13,6 +13,7 @@ CLI path.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -48,15 +49,19 @@ class StereoMatcher:
     (V, H) as volumes — written by the first pass of each direction, read by the
     other r-1 (ASW_DEN_*); bit-identical results, 2 more cost-sized buffers."""
 
-    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool = False,
+    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool | None = None,
                  otf: bool | None = None, support_index: bool | str | None = None):
         st = _lib.params_check(params)
         if st != _lib.ASW_OK:
             raise _lib.AswError(st, "asw_params_check")
         self.p = params.copy()
-        # asw_Aggr fused into the first V pass: bit-identical, but measured slower on
-        # MI355X (3.10 ms vs 2.02 + 0.64 ms, profiles/r01/kernel_stats_fused_raw.csv)
-        self.fuse_raw = fuse_raw
+        # asw_Aggr fused into the first V pass (k_vpass10_raw, asw_aggregate_pass_raw): the
+        # raw-cost volume is never written nor read; bit-identical, measured slower at C4
+        # (2.40 ms against 0.37 + 1.78, profiles/r04/fused_raw_r10d.log).  Default (None):
+        # off unless ASW_FUSE_RAW=1 (where built: ring tap counts, not a 32-plane shard)
+        if fuse_raw is None:
+            fuse_raw = os.environ.get("ASW_FUSE_RAW", "0") == "1"
+        self.fuse_raw = bool(fuse_raw) and K.raw_fused_supported(self.p)
         self.device = torch.device(device)
         dev = self.device
         self.lut = torch.empty(K.lut_shape(self.p), dtype=torch.float32, device=dev)

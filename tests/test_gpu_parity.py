@@ -177,7 +177,8 @@ def test_den_cache_write_then_read(gpu, oracle, T, direction, H, W, D, d0, d1):
 # multiple of 64), truncated AD, every den mode, and the den volume it writes
 @pytest.mark.parametrize("T", [5, 9, 33, 35, 51])
 @pytest.mark.parametrize("H,W,D,d0,d1,tau", [(37, 91, 70, 0, 70, 765.0), (23, 150, 200, 70, 135, 765.0),
-                                              (40, 77, 64, 0, 64, 90.0), (3, 5, 9, 0, 9, 765.0)])
+                                              (40, 77, 64, 0, 64, 90.0), (3, 5, 9, 0, 9, 765.0),
+                                              (150, 70, 64, 0, 64, 765.0), (233, 37, 200, 10, 140, 90.0)])
 def test_raw_fused_first_v_pass(gpu, oracle, T, H, W, D, d0, d1, tau):
     import torch
 
@@ -193,6 +194,8 @@ def test_raw_fused_first_v_pass(gpu, oracle, T, H, W, D, d0, d1, tau):
         den_b = den_a.clone()
         want = K.asw_vCostAggregation(p, wl, wr, c0, den=den_a, den_mode=mode)
         got = K.asw_vCostAggregation_raw(p, wl, wr, L, R, den=den_b, den_mode=mode)
+        # (the fused form of k_vpass10 at every ring tap count)
+        assert K.pass_kernel(0, mode).startswith(f"k_vpass10_raw<T={T},"), K.pass_kernel(0, mode)
         n = d1 - d0
         assert torch.equal(got[..., :n], want[..., :n]), (mode, torch.nonzero(got[..., :n] != want[..., :n])[:5])
         if mode == _lib.DEN_WRITE:
@@ -521,11 +524,13 @@ def test_c4_full_frame_oracle_parity(gpu, oracle):
     from stereo_matchin_amd.synthetic import make_pair
     W, H, D, T = 1920, 1080, 256, 35
     Lh, Rh, gt = make_pair(W, H, D, 0)
-    p, res = _run(gpu, Lh, Rh, D, T, 7)
+    p, res = _run(gpu, Lh, Rh, D, T, 7, fuse_raw=None)  # the matcher's default (as benched)
     names = _pass_kernels()
     print("C4 pass kernels:", names)
+    fused = StereoMatcher(p, gpu).fuse_raw  # asw_Aggr inside the first V pass (k_vpass10_raw)
     for dm in (1, 2):
-        assert names[(0, dm)].startswith(f"k_vpass10<T={T},NW=16,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
+        v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10"
+        assert names[(0, dm)].startswith(f"{v}<T={T},NW=16,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
         assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW=4,DM={dm}") and names[(1, dm)].endswith(",nt>"), \
             names
     ref = oracle.match(Lh, Rh, D, T, 7, want_cost=True)
@@ -552,11 +557,14 @@ def test_c5_band_oracle_parity(gpu, oracle):
     Lh, Rh, _ = make_pair(W, H, D, 3)
     Ls, Rs = np.ascontiguousarray(Lh[900:1170]), np.ascontiguousarray(Rh[900:1170])
     del Lh, Rh
-    _, res = _run(gpu, Ls, Rs, D, T, 7, lr_mode=1)
+    p, res = _run(gpu, Ls, Rs, D, T, 7, fuse_raw=None, lr_mode=1)
     names = _pass_kernels()
     print("C5 band pass kernels:", names)
+    from stereo_matchin_amd.kernels import raw_fused_supported
+    fused = raw_fused_supported(p)
     for dm in (1, 2):
-        assert names[(0, dm)].startswith(f"k_vpass10<T={T},NW=12,NPH=3,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
+        v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10"
+        assert names[(0, dm)].startswith(f"{v}<T={T},NW=12,NPH=3,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
         assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW={C5_H_NKW},DM={dm}") and \
             names[(1, dm)].endswith(",nt>"), names
     ref = oracle.match(Ls, Rs, D, T, 7, want_cost=True)
