@@ -88,11 +88,13 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
                                                    float *__restrict__ cost, int W, int Dp, int nloc, int d_begin,
                                                    float tau) {
     using f4 = float __attribute__((ext_vector_type(4)));
-    // R[y][xr], xr in [xlo, x0 + kRawSpan), element t at t + t/32: the lanes of a read
-    // are 4 elements apart (planes 4q..4q+3), so one pad dword per 32 puts the 32 lanes
-    // of a half-wave on 32 different banks (unpadded: 4-way conflicts)
+    // R[y][xr], xr in [xlo, x0 + kRawSpan), in 4 phases: element t at (t & 3) * s4 +
+    // (t >> 2).  The lanes of a read are 4 elements apart (planes 4q..4q+3 of lane q),
+    // so they read consecutive dwords of one phase (a linear row: 4-way conflicts), and
+    // s4 = 8 (mod 32) spreads the staging writes of 32 consecutive t over 32 banks.
     extern __shared__ uchar4 rrow[];
-    auto slot = [](int t) __attribute__((always_inline)) { return t + (t >> 5); };
+    const int s4 = ((kRawSpan + Dp - 1 + 3) / 4 + 31) / 32 * 32 + 8;
+    auto slot = [s4](int t) __attribute__((always_inline)) { return (t & 3) * s4 + (t >> 2); };
     const int y = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uchar4 *Lrow = L + (long long)y * W, *Rrow = R + (long long)y * W;
@@ -730,7 +732,7 @@ int asw_raw_cost(const asw_params *p, const uint8_t *left, const uint8_t *right,
     if (!left || !right || !cost) return ASW_E_INVALID;
     const int Dp = asw_disp_pitch(p);
     const dim3 grid((unsigned)((p->width + kRawSpan - 1) / kRawSpan), (unsigned)p->height);
-    const size_t lds = (size_t)((kRawSpan + Dp - 1) + (kRawSpan + Dp - 1) / 32 + 1) * 4;
+    const size_t lds = (size_t)4 * (((kRawSpan + Dp - 1 + 3) / 4 + 31) / 32 * 32 + 8) * 4;  // 4 phases of s4
     if (lds > 64 * 1024) return ASW_E_UNSUPPORTED;
     hipLaunchKernelGGL(k_raw_cost, grid, dim3(256), lds, (hipStream_t)stream, reinterpret_cast<const uchar4 *>(left),
                        reinterpret_cast<const uchar4 *>(right), cost, p->width, Dp, d_end_of(p) - p->d_begin,
