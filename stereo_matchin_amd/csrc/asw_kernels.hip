@@ -642,9 +642,9 @@ int asw_tune_set(int key, int value) {
     if (key == ASW_TUNE_PASS_VARIANT) {
         // only bits that select a compiled form (launch_dm): a stale bit would time the
         // default kernel under another name
-        // (+ bits 16-25: strip / segment counts, the lean H form and the index-form H
-        // phases of the 32-plane shard passes, asw_pass32.h)
-        if (value & ~(asw::kPassVariantBits | 0x3FF0000)) return ASW_E_INVALID;
+        // (+ bits 16-26: strip / segment counts, the lean H form and its ring, and the
+        // index-form H phases of the 32-plane shard passes, asw_pass32.h)
+        if (value & ~(asw::kPassVariantBits | 0x7FF0000)) return ASW_E_INVALID;
         return asw::set_pass_variant(value);
     }
     if (key == ASW_TUNE_WTA_VARIANT) {

@@ -375,9 +375,17 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     const rsrc_t rd = make_rsrc(den + rowoff);
     const int voff = pl * 4 + (y - 2 * pr) * W * kPlanes32 * 4;
     constexpr int xstride = kPlanes32 * 4;  // bytes per column
-    // LDS float4 index of this lane's entries at step x
-    auto wr_at = [&](int x) __attribute__((always_inline)) {
-        return myrow + ((x - d0 - pl + (1 << 20)) % RING) * Q;
+    // LDS float4 index of this lane's entries at step x.  The right slot (x - d0 - pl)
+    // mod RING is per lane: computed once per U-step chunk (rs0, at its first step xb),
+    // then slot(xb + s) = rs0 + s, less RING past the end (s <= U: at most two
+    // subtractions), instead of a modulo per request
+    static_assert(U < 2 * RING, "at most two wraps per chunk");
+    auto wr_slot0 = [&](int xb) __attribute__((always_inline)) { return (xb - d0 - pl + (1 << 20)) % RING; };
+    auto wr_at = [&](int rs0, int s) __attribute__((always_inline)) {
+        int v = rs0 + s;
+        v = v >= RING ? v - RING : v;
+        if (s >= RING) v = v >= RING ? v - RING : v;  // (s is a compile-time step)
+        return myrow + v * Q;
     };
     auto wl_at = [&](int x) __attribute__((always_inline)) { return myrow + (RING + x % LRING) * Q; };
 
@@ -391,14 +399,15 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 #pragma unroll
         for (int j = 0; j < KD; ++j) dring[j] = bload<CP>(rd, voff, min(xs + j, W - 1) * xstride);
     }
-    auto request = [&](auto kc, int x) __attribute__((always_inline)) {
+    // weights of phase k at step x = xb + s (rs0: the right slot at xb)
+    auto request = [&](auto kc, int x, int rs0, int s) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
         read_wr<T, PH::gb(k), PH::gb(k + 1)>(wlp[k], wl_at(x));
-        read_wr<T, PH::gb(k), PH::gb(k + 1)>(wrp[k], wr_at(x));
+        read_wr<T, PH::gb(k), PH::gb(k + 1)>(wrp[k], wr_at(rs0, s));
     };
-    request(std::integral_constant<int, 0>{}, xs);
+    request(std::integral_constant<int, 0>{}, xs, wr_slot0(xs), 0);
 
-    auto body = [&](auto sc, auto chk, int xb) __attribute__((always_inline)) {
+    auto body = [&](auto sc, auto chk, int xb, int rs0) __attribute__((always_inline)) {
         constexpr int s = decltype(sc)::value;
         constexpr bool CHK = decltype(chk)::value;
         const int x = xb + s;
@@ -429,8 +438,8 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
             wait_lgkm0();
             if constexpr (k == 0) asm volatile("" ::"v"(win[(s + T - 1) % U]));  // one vmcnt wait per step
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (k + 1 < NPH) request(std::integral_constant<int, k + 1>{}, x);
-            else request(std::integral_constant<int, 0>{}, x + 1);
+            if constexpr (k + 1 < NPH) request(std::integral_constant<int, k + 1>{}, x, rs0, s);
+            else request(std::integral_constant<int, 0>{}, x + 1, rs0, s + 1);
             __builtin_amdgcn_sched_barrier(0);
             taps32<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wlp[k], wrp[k], win);
             __builtin_amdgcn_sched_barrier(0);
@@ -446,9 +455,14 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
         win[(s + U - 1) % U] = bload<CP>(rc, voff, min(x + R + P, W - 1) * xstride);
     };
     int xb = xs;
-    for (; xb + U <= xe; xb += U)
-        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::false_type{}, xb); });
-    if (xb < xe) static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::true_type{}, xb); });
+    for (; xb + U <= xe; xb += U) {
+        const int rs0 = wr_slot0(xb);
+        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::false_type{}, xb, rs0); });
+    }
+    if (xb < xe) {
+        const int rs0 = wr_slot0(xb);
+        static_for<0, U>([&](auto sc) __attribute__((always_inline)) { body(sc, std::true_type{}, xb, rs0); });
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -540,9 +554,15 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         constexpr int NWB = T > 35 ? 2 : 4;
         if constexpr (T <= 35) {
             if (lean) {
-                // (one-wave blocks: 14.4 KB of LDS each, so 11 fit a CU)
-                if (stream) launch_h32<T, 1, DM, kCPStream, 4, false, 3>(p, wl, wr, cin, cout, den, st, seg);
-                else launch_h32<T, 1, DM, 0, 4, false, 3>(p, wl, wr, cin, cout, den, st, seg);
+                // (one-wave blocks: 14.4 KB of LDS each, so 11 fit a CU; variant bit 26: the
+                // conflict-free 48-entry ring, 16.7 KB, 9 per CU)
+                if (g_pass_variant & (1 << 26)) {
+                    if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
+                    else launch_h32<T, 1, DM, 0, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
+                } else {
+                    if (stream) launch_h32<T, 1, DM, kCPStream, 4, false, 3>(p, wl, wr, cin, cout, den, st, seg);
+                    else launch_h32<T, 1, DM, 0, 4, false, 3>(p, wl, wr, cin, cout, den, st, seg);
+                }
                 return finish32();
             }
         }
