@@ -80,6 +80,10 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="with --api frame: asw_set_graph (the device work replayed from HIP graphs)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="stream the frames through two sets of volumes: frame k's WTA tail (the RCCL exchange, "
+                         "target scan, LR check) on a side stream overlapping frame k+1's aggregation "
+                         "(distributed.PipelinedMatcher; stage API)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--group-size", type=int, default=0,
                     help="ranks per d-sharded frame (0: one frame over all ranks; the plan_groups layout is timed "
@@ -230,7 +234,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     from stereo_matchin_amd import FrameContext, make_params
-    from stereo_matchin_amd.distributed import ShardedStereoMatcher, plan_groups
+    from stereo_matchin_amd.distributed import PipelinedMatcher, ShardedStereoMatcher, plan_groups
     from stereo_matchin_amd.pipeline import StereoMatcher
 
     W, H, D, T, iters, lr, desc = WORKLOADS[args.workload]
@@ -258,7 +262,12 @@ def main():
         nloc = D
     else:
         pairs = [(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)) for L, R in pairs_h]
-        if G > 1:
+        if args.pipeline:
+            if REFINE.get(args.workload, 0):
+                raise SystemExit("--pipeline: workloads without the refinement loop")
+            m = PipelinedMatcher(p, grank, G, dev, group=pg)
+            nloc = m.p.d_stop - m.p.d_begin
+        elif G > 1:
             m = ShardedStereoMatcher(p, grank, G, dev, group=pg)
             nloc = m.p.d_stop - m.p.d_begin
         else:
@@ -278,7 +287,7 @@ def main():
                 spans.append(out["timings"])
             else:
                 ev = [] if events is not None else None
-                res = m.match(*pairs[b], events=ev)
+                res = m.submit(*pairs[b], events=ev) if args.pipeline else m.match(*pairs[b], events=ev)
                 if k_ref:  # main.cpp:540-623: k x (ref_v, ref_h, WTA_REF, LR) + 3x3 median
                     from stereo_matchin_amd import _lib
                     m.refine(res, *pairs[b], rp=_lib.default_refine_params(iters=k_ref))
@@ -291,6 +300,8 @@ def main():
     for _ in range(args.warmup):
         step()
     spans.clear()
+    if args.pipeline:
+        m.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -300,6 +311,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(evs)
+    if args.pipeline:
+        m.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -340,7 +353,7 @@ def main():
     # the faster): one V and one H pass without the cached denominators, on the
     # matcher's own buffers, after the timed region (not part of `value`)
     v_none, h_none = [], []
-    if not frame and world == 1 and iters >= 2:
+    if not frame and not args.pipeline and world == 1 and iters >= 2:
         from stereo_matchin_amd import kernels as K
         for _ in range(3):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -419,7 +432,7 @@ def main():
             "config": {"workload": desc, "width": W, "height": H, "ndisp": D, "taps": T, "iters": iters,
                        "lr_check": lr, "lr_mode": "native" if lr_mode else "u8", "pairs_per_step": batch,
                        "local_planes": nloc, "frames_per_step": groups * batch,
-                       "api": args.api + ("+graph" if frame and args.graph else ""),
+                       "api": args.api + ("+graph" if frame and args.graph else "") + ("+pipeline" if args.pipeline else ""),
                        "parallelism": (f"{groups} frame group(s), each d-sharded over {G} GPU(s)"
                                        if world > 1 else "single GPU")},
             "roofline": {"bound": "hbm", "achieved": round(gbs(dom_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -72,9 +72,10 @@ def _allreduce_min_factory(group=None) -> Callable[[torch.Tensor], torch.Tensor]
     return reduce_min
 
 
-def sharded_wta(ops: ShardOps, cost, reduce_min: Callable) -> tuple:
-    """Exact WTA over a d-sharded cost volume (see module doc)."""
-    key, m1, m2 = ops.local(cost)
+def sharded_wta(ops: ShardOps, cost, reduce_min: Callable, local: tuple | None = None) -> tuple:
+    """Exact WTA over a d-sharded cost volume (see module doc).  ``local``: the
+    (key, m1, m2) of ops.local(cost) when already computed."""
+    key, m1, m2 = ops.local(cost) if local is None else local
     key_g = reduce_min(key.clone())
     m2_g = reduce_min(ops.second(key_g, key, m1, m2))
     tkey, t1, t2 = ops.target_local(cost, key_g)
@@ -139,3 +140,77 @@ def _record():
     e = torch.cuda.Event(enable_timing=True)
     e.record()
     return e
+
+
+class PipelinedMatcher:
+    """Frames streamed through ``depth`` sets of volumes, the WTA tail of frame k
+    overlapping the aggregation of frame k+1.
+
+    The main stream runs frame k's raw cost, supports, 2r passes and the local WTA scan
+    (``asw_wta_local``); a side stream then runs the rest of its WTA — on a d-sharded
+    frame the four MIN all-reduces over RCCL with the target scan between them
+    (``sharded_wta``), on a whole-range frame ``asw_WTA`` itself — and the consistency
+    check, while the main stream goes on with frame k+1 in the other set of volumes.
+    A set is reused only after its frame's tail has finished (an event the main stream
+    waits for).  Results are bit-identical to ``ShardedStereoMatcher.match`` /
+    ``StereoMatcher.match`` (tests/test_gpu_frame.py, tests/test_distributed.py).
+
+    ``submit(left, right)`` returns the frame's ``MatchResult`` (valid once ``flush()``
+    or a later ``submit`` into the same set has ordered the caller's stream after it:
+    ``flush()`` makes the current stream wait for every submitted tail)."""
+
+    def __init__(self, params: AswParams, rank: int = 0, world: int = 1, device="cuda", group=None, depth: int = 2):
+        self.device = torch.device(device)
+        self.sharded = world > 1
+        if self.sharded:
+            self.sets = [ShardedStereoMatcher(params, rank, world, self.device, group) for _ in range(depth)]
+            self.p = self.sets[0].p
+        else:
+            self.sets = [StereoMatcher(params, self.device) for _ in range(depth)]
+            self.p = self.sets[0].p
+        self.side = torch.cuda.Stream(self.device)
+        self.done: list = [None] * depth
+        self.k = 0
+
+    def submit(self, left: torch.Tensor, right: torch.Tensor, events: list | None = None) -> MatchResult:
+        """Queue one frame.  ``events``: ("start", "support", "v"/"h" per pass) on the main
+        stream and ("consistency") at the end of its tail on the side stream."""
+        i = self.k % len(self.sets)
+        self.k += 1
+        main = torch.cuda.current_stream(self.device)
+        if self.done[i] is not None:
+            main.wait_event(self.done[i])  # set i's previous tail has finished with its volume
+        st = self.sets[i]
+        m = st.matcher if self.sharded else st
+        if events is not None:
+            events.append(("start", _record()))
+        fuse = m.fuse_raw and m.p.iters >= 1
+        m.raw_and_support(left, right, raw=not fuse)
+        if events is not None:
+            events.append(("support", _record()))
+        cost = m.aggregate(events, images=(left, right) if fuse else None)
+        local = st.ops.local(cost) if self.sharded else None
+        ready = torch.cuda.Event()
+        ready.record(main)
+        p = m.p
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ready)
+            for t in (local or ()):
+                t.record_stream(self.side)
+            if self.sharded:
+                d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = sharded_wta(st.ops, cost, st.reduce_min, local)
+            else:
+                d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.asw_WTA(p, cost)
+            lr = red = None
+            if p.lr_check:
+                lr, red = K.Constistency(p, d_ref, d_tar, code_ref, code_tar, conf_ref, conf_tar)
+            done = torch.cuda.Event(enable_timing=events is not None)
+            done.record(self.side)
+        if events is not None:
+            events.append(("consistency", done))
+        self.done[i] = done
+        return MatchResult(d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, lr, red, cost)
+
+    def flush(self) -> None:
+        """Order the current stream after every submitted frame's tail."""
+        torch.cuda.current_stream(self.device).wait_stream(self.side)
