@@ -19,7 +19,12 @@ and runs the half-wave passes of asw_pass32.h): "scaling": "strong", the frame's
 total work is fixed.  ``--group-size G`` splits the N ranks into N/G concurrent
 frames of G shards instead; without it, the layout with the most maps/s,
 plan_groups(D, N) ranks per frame, is timed after the main run and reported beside
-``value`` as ``frame_groups`` (not as ``value``).
+``value`` as ``frame_groups`` (not as ``value``).  On N > 1 the frames are streamed
+(``--pipeline``, default on there): frame k's WTA tail — the four RCCL all-reduces with
+the target scan between them, and the LR check — runs on a side stream while frame
+k+1 aggregates in a second set of volumes (distributed.PipelinedMatcher), so the
+exchange is hidden behind the next frame's passes; every frame's work is inside the
+timed region (the side stream is joined before the closing synchronize).
 
 Rank 0 prints ONE JSON line.  ``roofline`` is the dominant kernel: the V
 aggregation pass with cached denominators (k_vpass10, DEN_READ: r-1 of the 2r
@@ -80,10 +85,11 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="with --api frame: asw_set_graph (the device work replayed from HIP graphs)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--pipeline", action="store_true",
+    ap.add_argument("--pipeline", default="auto", choices=["auto", "on", "off"],
                     help="stream the frames through two sets of volumes: frame k's WTA tail (the RCCL exchange, "
                          "target scan, LR check) on a side stream overlapping frame k+1's aggregation "
-                         "(distributed.PipelinedMatcher; stage API)")
+                         "(distributed.PipelinedMatcher; stage API).  auto: on for N > 1 (it hides the exchange), "
+                         "off on one GPU (measured the same there: 23.63 vs 23.59 ms, profiles/r04/pipeline_r10h.log)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--group-size", type=int, default=0,
                     help="ranks per d-sharded frame (0: one frame over all ranks; the plan_groups layout is timed "
@@ -257,14 +263,14 @@ def main():
         [(L, R) for L, R in load_pairs(args.workload, W, H, D, batch * groups)][gid * batch:(gid + 1) * batch]
     p = make_params(W, H, ndisp=D, taps=T, iters=iters, lr_check=int(lr), lr_mode=lr_mode)
     frame = args.api == "frame"
+    args.pipeline = not frame and not REFINE.get(args.workload, 0) and (
+        args.pipeline == "on" or (args.pipeline == "auto" and world > 1))
     if frame:
         fc = FrameContext(p, devices=[local], graph=args.graph)
         nloc = D
     else:
         pairs = [(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)) for L, R in pairs_h]
         if args.pipeline:
-            if REFINE.get(args.workload, 0):
-                raise SystemExit("--pipeline: workloads without the refinement loop")
             m = PipelinedMatcher(p, grank, G, dev, group=pg)
             nloc = m.p.d_stop - m.p.d_begin
         elif G > 1:
