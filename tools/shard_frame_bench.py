@@ -23,14 +23,16 @@ def main():
     ap.add_argument("--world", type=int, default=4)
     ap.add_argument("--rank", type=int, default=1)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5"],
+                    help="c4: 1920x1080 D256 T35; c5: 3840x2160 D512 T51 (native LR)")
     ap.add_argument("--support-index", default="", choices=["", "1", "v"],
                     help="index-form supports (asw_aggregate_pass_index): both directions, or V only (A/B)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    W, H, D, T, r = 1920, 1080, 256, 35, 7
+    W, H, D, T, r = (1920, 1080, 256, 35, 7) if a.workload == "c4" else (3840, 2160, 512, 51, 7)
     Lh, Rh, _ = make_pair(W, H, D, 0)
     L, R = torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev)
-    p = make_params(W, H, ndisp=D, taps=T, iters=r, lr_check=1)
+    p = make_params(W, H, ndisp=D, taps=T, iters=r, lr_check=1, lr_mode=1 if D > 256 else 0)
     m = ShardedStereoMatcher(p, a.rank, a.world, dev, support_index={"": None, "1": True, "v": "v"}[a.support_index])
     m.match(L, R)
     torch.cuda.synchronize()
@@ -39,7 +41,7 @@ def main():
         m.match(L, R)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / a.reps
-    print(json.dumps({"world": a.world, "rank": a.rank, "planes": m.p.d_stop - m.p.d_begin,
+    print(json.dumps({"workload": a.workload, "world": a.world, "rank": a.rank, "planes": m.p.d_stop - m.p.d_begin,
                       "support_index": {"v": m.matcher.vidx, "h": m.matcher.hidx},
                       "ms_per_shard_frame_no_collective": round(ms, 3)}))
 
