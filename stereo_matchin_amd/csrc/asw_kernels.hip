@@ -148,14 +148,25 @@ struct SupportJobs {
     int dir[4];
     int idx[4];   // 1: write the LUT index dist*766 + SAD of each weight (asw_support_all_fmt)
 };
-template <int Q>
+// EXPD: each weight computed as k_support_lut computes the table entry, (float)
+// exp_d((double)(c_diff[SAD] - g_dist[dist])) with the two float quotients tabulated
+// per block in LDS (766 + R+1 entries), instead of gathered from the LUT: the same
+// value bit for bit, no dependent image -> LUT gather chain (~20 double-precision
+// VALU per weight instead).
+template <int Q, bool EXPD = false>
 __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *__restrict__ lut, int W, int H,
-                                                 int T) {
+                                                 int T, float gamma_c = 1.0f, float gamma_g = 1.0f) {
     using f4 = float __attribute__((ext_vector_type(4)));
     // 4 waves x 64 pixels x Q float4 = 4 KiB per Q: Q = 17 (T 65-68) takes 68 KiB,
     // which only the 160 KiB LDS of gfx950 holds (the build targets gfx950 only)
     static_assert(4 * 64 * Q * 16 <= 160 * 1024, "k_support staging tile exceeds the gfx950 LDS");
     __shared__ f4 stg[4][64 * Q];  // per wave: its 64 pixels' Q float4, in output order
+    __shared__ float cd_s[EXPD ? kLutWidth : 1], gd_s[EXPD ? 2 * Q + 1 : 1];  // (R <= 2Q)
+    if constexpr (EXPD) {  // (before any wave leaves: the one barrier)
+        for (int t = threadIdx.x; t < kLutWidth; t += 256) cd_s[t] = (float)(-t) / gamma_c;  // K/asw_vsupport.cl:22
+        for (int t = threadIdx.x; t <= T / 2; t += 256) gd_s[t] = (float)t / gamma_g;        // :24
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x0 = blockIdx.x * 64;
     const int y = blockIdx.y * 4 + wv;
@@ -223,7 +234,8 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
                 dist = x > qx ? x - qx : qx - x;
             }
             const int sad = abs((int)a.x - (int)b[k].x) + abs((int)a.y - (int)b[k].y) + abs((int)a.z - (int)b[k].z);
-            v[k / 4][k % 4] = k < T ? lut[dist * kLutWidth + sad] : 0.0f;
+            if constexpr (EXPD) v[k / 4][k % 4] = k < T ? (float)exp_d((double)(cd_s[sad] - gd_s[dist])) : 0.0f;
+            else v[k / 4][k % 4] = k < T ? lut[dist * kLutWidth + sad] : 0.0f;
         }
         // The wave's 64 pixels are one contiguous 64*Q-float4 run of the output:
         // transposed through LDS (Q odd: the 144-B lane stride of the writes is
@@ -277,11 +289,18 @@ __global__ __launch_bounds__(256) void k_support_any(SupportJobs jobs, const flo
     reinterpret_cast<f4 *>(jobs.w[blockIdx.z] + (long long)y * W * Tp)[t] = v;
 }
 
+// asw_tune_set(ASW_TUNE_PASS_VARIANT) bit 27: k_support computes each weight's exp
+// instead of gathering it from the LUT (EXPD)
+int g_support_expd = 0;
 template <int Q>
 void launch_support_q(const asw_params *p, const SupportJobs &jobs, int njobs, const float *lut,
                              hipStream_t st) {
     const dim3 grid((unsigned)((p->width + 63) / 64), (unsigned)((p->height + 3) / 4), (unsigned)njobs);
-    hipLaunchKernelGGL(k_support<Q>, grid, dim3(256), 0, st, jobs, lut, p->width, p->height, p->taps);
+    if (g_support_expd)
+        hipLaunchKernelGGL((k_support<Q, true>), grid, dim3(256), 0, st, jobs, lut, p->width, p->height, p->taps,
+                           p->gamma_c, p->gamma_g);
+    else hipLaunchKernelGGL((k_support<Q, false>), grid, dim3(256), 0, st, jobs, lut, p->width, p->height, p->taps,
+                            p->gamma_c, p->gamma_g);
 }
 
 // ---------------------------------------------------------------------------
@@ -644,8 +663,11 @@ int asw_tune_set(int key, int value) {
         // default kernel under another name
         // (+ bits 16-26: strip / segment counts, the lean H form and its ring, and the
         // index-form H phases of the 32-plane shard passes, asw_pass32.h)
-        if (value & ~(asw::kPassVariantBits | 0x7FF0000)) return ASW_E_INVALID;
-        return asw::set_pass_variant(value);
+        // (bit 27: the support kernel's EXPD form, k_support)
+        if (value & ~(asw::kPassVariantBits | 0xFFF0000)) return ASW_E_INVALID;
+        const int old_expd = asw::g_support_expd;
+        asw::g_support_expd = (value >> 27) & 1;
+        return asw::set_pass_variant(value & ~(1 << 27)) | (old_expd << 27);
     }
     if (key == ASW_TUNE_WTA_VARIANT) {
         if (value < 0 || value > 2) return ASW_E_INVALID;

@@ -56,3 +56,17 @@ def gpu():
     import stereo_matchin_amd._lib as L
     L.lib()  # loud failure if the HIP library is missing
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def tune_variant():
+    """asw_tune_set(ASW_TUNE_PASS_VARIANT, v) for one test, restored afterwards."""
+    from stereo_matchin_amd import _lib
+    saved = []
+
+    def set_(v):
+        saved.append(_lib.lib().asw_tune_set(1, v))
+
+    yield set_
+    if saved:
+        _lib.lib().asw_tune_set(1, saved[0])

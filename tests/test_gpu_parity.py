@@ -83,8 +83,11 @@ def test_raw_cost_truncated(gpu, oracle):
 # pair is ragged (W not a multiple of 64, H of 4)
 @pytest.mark.parametrize("T", [1, 3, 5, 17, 33, 35, 41, 51, 57, 65, 71])
 @pytest.mark.parametrize("scene", ["tsukuba", "ragged"])
-def test_support(gpu, oracle, T, scene):
+@pytest.mark.parametrize("expd", [False, True])  # variant bit 27: k_support computes exp_d itself
+def test_support(gpu, oracle, T, scene, expd, tune_variant):
     import stereo_matchin_amd.kernels as K
+    if expd:
+        tune_variant(1 << 27)
     if scene == "tsukuba":
         Lh, Rh, _ = load_scene("tsukuba")
     else:

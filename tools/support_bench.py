@@ -22,12 +22,14 @@ from stereo_matchin_amd.synthetic import make_pair  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0")
+    ap.add_argument("--variants", default="0,134217728",
+                    help="asw_tune_set(ASW_TUNE_PASS_VARIANT) values; bit 27: k_support computes exp itself")
+    ap.add_argument("--c5", action="store_true", help="3840x2160 (default 1920x1080)")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--taps", type=int, default=35)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    W, H = 1920, 1080
+    W, H = (3840, 2160) if a.c5 else (1920, 1080)
     Lh, Rh, _ = make_pair(W, H, 256, 0)
     p = make_params(W, H, ndisp=256, taps=a.taps, iters=1)
     L, R = torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev)
@@ -36,7 +38,7 @@ def main():
     lib = _lib.lib()
     ref = None
     for v in [int(x) for x in a.variants.split(",")]:
-        old = lib.asw_tune_set(2, v)
+        old = lib.asw_tune_set(1, v)
         ts = []
         for r in range(a.reps + 1):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -46,7 +48,7 @@ def main():
             torch.cuda.synchronize()
             if r:
                 ts.append(e0.elapsed_time(e1))
-        lib.asw_tune_set(2, old)
+        lib.asw_tune_set(1, old)
         got = [w.clone() for w in ws]
         same = ref is None or all(torch.equal(g, q) for g, q in zip(got, ref))
         ref = ref or got
