@@ -381,16 +381,25 @@ def main():
     if 1 < g2 < world:
         subs2 = [dist.new_group(list(range(g * g2, (g + 1) * g2)), backend="gloo" if rehearsal else None)
                  for g in range(world // g2)]
-        m2 = ShardedStereoMatcher(p, rank % g2, g2, dev, group=subs2[rank // g2])
+        if args.pipeline:  # (streamed like the main run)
+            m2 = PipelinedMatcher(p, rank % g2, g2, dev, group=subs2[rank // g2])
+            run2 = m2.submit
+        else:
+            m2 = ShardedStereoMatcher(p, rank % g2, g2, dev, group=subs2[rank // g2])
+            run2 = m2.match
         for _ in range(2):
             for b in range(batch):
-                m2.match(*pairs[b])
+                run2(*pairs[b])
+        if args.pipeline:
+            m2.flush()
         torch.cuda.synchronize()
         dist.barrier()
         t1 = time.perf_counter()
         for _ in range(args.steps):
             for b in range(batch):
-                m2.match(*pairs[b])
+                run2(*pairs[b])
+        if args.pipeline:
+            m2.flush()
         torch.cuda.synchronize()
         dist.barrier()
         el2 = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
