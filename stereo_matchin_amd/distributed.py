@@ -209,7 +209,11 @@ class PipelinedMatcher:
         if events is not None:
             events.append(("consistency", done))
         self.done[i] = done
-        return MatchResult(d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, lr, red, cost)
+        outs = (d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar, lr, red)
+        for t in outs:  # allocated on the side stream, read on the caller's: freed after both
+            if t is not None:
+                t.record_stream(main)
+        return MatchResult(*outs, cost)
 
     def flush(self) -> None:
         """Order the current stream after every submitted frame's tail."""
