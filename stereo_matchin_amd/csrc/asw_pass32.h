@@ -178,8 +178,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     (void)r1;
     request(std::integral_constant<int, 0>{}, 0);
 
-    auto chunk = [&](auto clamp_c, int ys) __attribute__((always_inline)) {
-        constexpr bool CLAMP = decltype(clamp_c)::value;
+    // mode 0: interior chunk; 1: clamped row addresses; 2: clamped and partial (rows >= y_end skipped)
+    auto chunk = [&](auto mode_c, int ys) __attribute__((always_inline)) {
+        constexpr bool CLAMP = decltype(mode_c)::value >= 1;
+        constexpr bool PART = decltype(mode_c)::value == 2;
         const int cb = min(ys + R + P, H - 1);
         const rsrc_t rc = rsrc_at(cin, cb);
         const rsrc_t ro = rsrc_at(cout, ys);
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
         static_for<0, U>([&](auto sc) __attribute__((always_inline)) {
             constexpr int s = decltype(sc)::value;
             const int y = ys + s;
-            if constexpr (CLAMP) {
+            if constexpr (PART) {
                 if (y >= y_end) return;
             }
             constexpr int bcur = s % NBUF, bnext = (s + 1) % NBUF, bput = (s + LEAD) % NBUF;
@@ -232,11 +234,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
         });
     };
     int ys = y_begin;
-    for (; ys + U <= y_end && ys + U - 1 + LA <= H - 1; ys += U) chunk(std::false_type{}, ys);
-    for (; ys < y_end; ys += U) {  // the chunks that reach the image bottom, and the partial last chunk
+    for (; ys + U <= y_end && ys + U - 1 + LA <= H - 1; ys += U) chunk(std::integral_constant<int, 0>{}, ys);
+    // whole chunks that reach the image bottom, then the partial last one (k_vpass10)
+    for (; ys + U <= y_end; ys += U) {
         asm volatile("" : "+s"(ys));
-        chunk(std::true_type{}, ys);
+        chunk(std::integral_constant<int, 1>{}, ys);
     }
+    if (ys < y_end) chunk(std::integral_constant<int, 2>{}, ys);
 }
 
 // ---------------------------------------------------------------------------
