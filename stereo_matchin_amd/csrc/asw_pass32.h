@@ -327,16 +327,22 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
             return a;
         }
     };
-    const elem_t *st_row[SPL];
-    int st_q4[SPL], st_k[SPL], st_kind[SPL], st_slot[SPL], st_base[SPL];
+    // (the share's row is a global-address-space pointer: a generic one compiles to
+    // flat loads, which also count against lgkmcnt, so every LDS wait of the step loop
+    // would wait for the staging loads of the next batch as well; the clamp is the
+    // same arithmetic for both kinds, st_sub = d0 or 0, so no branch either)
+    using gelem_t = const __attribute__((address_space(1))) elem_t;
+    gelem_t *st_row[SPL];
+    int st_q4[SPL], st_k[SPL], st_kind[SPL], st_sub[SPL], st_slot[SPL], st_base[SPL];
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
         const int n = min(j * 64 + lane, NST - 1);
         const int q = n % Q, k = (n / Q) % K, kind = (n / (Q * K)) & 1, r = n / (2 * Q * K);
-        st_row[j] = kind == 0 ? wrrows[r] : wlrows[r];
+        st_row[j] = (gelem_t *)(kind == 0 ? wrrows[r] : wlrows[r]);
         st_q4[j] = 4 * q;
         st_k[j] = k;
         st_kind[j] = kind;
+        st_sub[j] = kind == 0 ? d0 : 0;
         // LDS float4 index of the entry for the first top (xb = xs: entries of batch xs + K)
         const int e = xs + K + 1 + k;
         st_slot[j] = kind == 0 ? (r * ROWE + (e - d0 + (1 << 20)) % RING) * Q + q
@@ -344,9 +350,8 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
         st_base[j] = kind == 0 ? r * ROWE * Q : (r * ROWE + RING) * Q;
     }
     auto st_load = [&](int j, int xb) __attribute__((always_inline)) {  // entry of the batch starting at xb
-        const int e = xb + 1 + st_k[j];
-        const int c = st_kind[j] == 0 ? clampi(e - d0, 0, W - 1) : min(e, W - 1);
-        return *reinterpret_cast<const stg_t *>(st_row[j] + c * TP + st_q4[j]);
+        const int c = clampi(xb + 1 + st_k[j] - st_sub[j], 0, W - 1);  // (left: xb + 1 + k >= 0)
+        return *reinterpret_cast<const __attribute__((address_space(1))) stg_t *>(st_row[j] + c * TP + st_q4[j]);
     };
 
     // the rings before step xs: right entries [xs-d0-31, xs+K-d0], left [xs, xs+K]
