@@ -290,10 +290,13 @@ int alloc_shard(Shard &s, bool sharded) {
     ASWCHK(dev_alloc(&s.c0, asw_cost_bytes(p)));
     ASWCHK(dev_alloc(&s.c1, asw_cost_bytes(p)));
     if (p->iters >= 2) {  // the den of a direction is written by its first pass and read by the r-1 others
-        // (a 32-plane shard's V pass recomputes it: k_vpass32 den-none 0.32 against den-read
-        // 0.36 ms at C4 / 8, profiles/r04; its H pass reads it)
-        if (asw_disp_pitch(p) != 32) ASWCHK(dev_alloc(&s.den_v, asw_cost_bytes(p)));
-        ASWCHK(dev_alloc(&s.den_h, asw_cost_bytes(p)));
+        // (a 32-plane shard's passes recompute it: at C4 / 8 k_vpass32 den-none 0.24 against
+        // den-read 0.28 ms, k_hpass32 0.30-0.33 against 0.36, profiles/r04/h32_variants_r11d.log;
+        // ASW_SHARD_DEN_H=1 keeps the H pass reading it)
+        const char *denh_env = std::getenv("ASW_SHARD_DEN_H");
+        const bool p32 = asw_disp_pitch(p) == 32;
+        if (!p32) ASWCHK(dev_alloc(&s.den_v, asw_cost_bytes(p)));
+        if (!p32 || (denh_env && denh_env[0] == '1')) ASWCHK(dev_alloc(&s.den_h, asw_cost_bytes(p)));
     }
     if (sharded) {
         ASWCHK(dev_alloc(&s.key, S * 8));

@@ -93,11 +93,15 @@ class StereoMatcher:
         self.c1 = K.new_cost(self.p, dev)
         self.den_v = self.den_h = None
         if den_cache and self.p.iters >= 2:
-            # a 32-plane shard's V pass recomputes den (k_vpass32: den-none 0.32 against
-            # den-read 0.36 ms at C4 / 8), its H pass reads it (asw_frame.cpp the same)
-            if K.cost_shape(self.p)[2] != 32:
+            # a 32-plane shard's passes recompute den (C4 / 8: k_vpass32 den-none 0.24
+            # against den-read 0.28 ms, k_hpass32 0.30-0.33 against 0.36,
+            # profiles/r04/h32_variants_r11d.log; ASW_SHARD_DEN_H=1 keeps the H pass
+            # reading it; asw_frame.cpp the same)
+            p32 = K.cost_shape(self.p)[2] == 32
+            if not p32:
                 self.den_v = K.new_cost(self.p, dev)
-            self.den_h = K.new_cost(self.p, dev)
+            if not p32 or os.environ.get("ASW_SHARD_DEN_H", "0") == "1":
+                self.den_h = K.new_cost(self.p, dev)
 
     # -- stages ---------------------------------------------------------------
     def raw_and_support(self, left: torch.Tensor, right: torch.Tensor, raw: bool = True):

@@ -100,7 +100,7 @@ def test_pass32_rejects_fused_raw_and_otf(gpu):
 # the C4 shard of the 8-way split: one rank's 32 planes of a 1920-column D256 T35
 # frame through the whole r = 7 pass sequence, on a full-width band of 215 rows (the
 # oracle's passes over all 1080 rows take minutes), against the oracle on that band
-def test_c4_shard_band_r7(gpu, oracle):
+def test_c4_shard_band_r7(gpu, oracle, monkeypatch):
     import stereo_matchin_amd.kernels as K
     from stereo_matchin_amd.pipeline import StereoMatcher
     from stereo_matchin_amd.synthetic import make_pair
@@ -116,17 +116,21 @@ def test_c4_shard_band_r7(gpu, oracle):
     for _ in range(r):
         cost = oracle.aggregate_pass(*sv, cost, T, 0, d0=d0, d1=d1, plane_base=d0)
         cost = oracle.aggregate_pass(*sh, cost, T, 1, d0=d0, d1=d1, plane_base=d0)
-    # float supports (the default), then index-form supports (opt-in)
-    for index in (None, True):
+    # float supports (the default), index-form supports (opt-in), and
+    # float supports with the H denominators cached (ASW_SHARD_DEN_H=1)
+    for index, denh in ((None, "0"), (True, "0"), (None, "1")):
+        monkeypatch.setenv("ASW_SHARD_DEN_H", denh)
         m = StereoMatcher(p, gpu, support_index=index)
         m.raw_and_support(_t(Lb, gpu), _t(Rb, gpu))
         got = plane_major(_np(m.aggregate()), d1 - d0)
-        # (a 32-plane shard recomputes the V denominators, caches the H ones)
+        # (a 32-plane shard recomputes the denominators of both directions by default)
         tag = ",IDX" if index else ""
         assert m.vidx == m.hidx == bool(index)
         assert K.pass_kernel(0, 0).startswith("k_vpass32<T=35,NW=16,NPH=4" + tag), K.pass_kernel(0, 0)
-        assert K.pass_kernel(1, 2).startswith("k_hpass32<T=35,NWB=" + ("8,NPH=4,IDX" if index else "1,NPH=4"))
-        assert np.array_equal(got, cost), (index, np.argwhere(got != cost)[:5])
+        assert (m.den_h is not None) == (denh == "1")
+        assert K.pass_kernel(1, 2 if denh == "1" else 0).startswith(
+            "k_hpass32<T=35,NWB=" + ("8,NPH=4,IDX" if index else "1,NPH=4")), K.pass_kernel(1, 0)
+        assert np.array_equal(got, cost), (index, denh, np.argwhere(got != cost)[:5])
         del m
 
 
