@@ -549,9 +549,9 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         // 640-column segments, 1620 waves (four segments, 2160 waves, left a tail round
         // of 112 waves); the window prologue (U-1 columns) is paid once per segment.
         // Variant bits 20-23 (asw_tune_set) override the segment count.
-        // T <= 35: the "lean" form, 4 weight phases and the minimal right ring (138
-        // VGPRs, 14.4 KB of LDS per one-wave block: up to 11 waves per CU against 8):
-        // C4 / 8 den-read 0.326 against 0.358 ms (profiles/r04/pass32_h_r09e.log).  Variant
+        // T <= 35: the "lean" form, 4 weight phases in one-wave blocks (138 VGPRs, up to
+        // 9-11 waves per CU against 8): C4 / 8 den-read 0.326 against 0.358 ms
+        // (profiles/r04/pass32_h_r09e.log).  Variant
         // bit 24 selects the 4-wave-block form instead.
         const bool lean = T <= 35 && !(g_pass_variant & (1 << 24));
         const int pairs = (p->height + 1) / 2;
@@ -563,9 +563,11 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         constexpr int NWB = T > 35 ? 2 : 4;
         if constexpr (T <= 35) {
             if (lean) {
-                // (one-wave blocks: 14.4 KB of LDS each, so 11 fit a CU; variant bit 26: the
-                // conflict-free 48-entry ring, 16.7 KB, 9 per CU)
-                if (g_pass_variant & (1 << 26)) {
+                // (one-wave blocks with the conflict-free 48-entry ring, 16.7 KB of LDS, 9 per
+                // CU: C4 8-way shard frame 4.73 against 4.81-4.98 ms with the minimal 40-entry
+                // ring, 14.4 KB, 11 per CU, profiles/r04/shard_variants_r11g.log; variant bit
+                // 26 selects the minimal ring)
+                if (!(g_pass_variant & (1 << 26))) {
                     if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
                     else launch_h32<T, 1, DM, 0, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
                 } else {

@@ -37,7 +37,7 @@ def test_tune_set_rejects_bits_that_select_nothing(L):
     lib = L.lib()
     assert lib.asw_tune_set(1, 64) == L.ASW_E_INVALID      # round 1's 10-wave H form: no longer built
     assert lib.asw_tune_set(1, 1 << 28) == L.ASW_E_INVALID
-    assert lib.asw_tune_set(1, 1 << 26) == 0 and lib.asw_tune_set(1, 0) == 1 << 26  # the lean H32 ring (asw_pass32.h)
+    assert lib.asw_tune_set(1, 1 << 26) == 0 and lib.asw_tune_set(1, 0) == 1 << 26  # the minimal lean H32 ring (asw_pass32.h)
     assert lib.asw_tune_set(1, 1 << 27) == 0 and lib.asw_tune_set(1, 0) == 1 << 27  # k_support's EXPD form
     assert lib.asw_tune_set(2, 5) == L.ASW_E_INVALID
     old = lib.asw_tune_set(1, 128)

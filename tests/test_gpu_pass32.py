@@ -82,6 +82,16 @@ def test_pass32_bit_exact(gpu, oracle, T, direction, H, W, D, d0, d1):
             assert name.startswith("k_pass_any<"), name
 
 
+# the other H forms behind variant bits (asw_pass32.h): bit 26 = the minimal 40-entry
+# lean ring (the default is the 48-entry one), bit 24 = the 4-wave-block form
+@pytest.mark.parametrize("variant", [1 << 26, 1 << 24])
+@pytest.mark.parametrize("T", [9, 35])
+@pytest.mark.parametrize("H,W,D,d0,d1", [(37, 91, 70, 38, 70), (9, 331, 256, 224, 256)])
+def test_pass32_h_variants_bit_exact(gpu, oracle, tune_variant, variant, T, H, W, D, d0, d1):
+    tune_variant(variant)
+    test_pass32_bit_exact(gpu, oracle, T, 1, H, W, D, d0, d1)
+
+
 def test_pass32_rejects_fused_raw_and_otf(gpu):
     import torch
 

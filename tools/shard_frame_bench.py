@@ -2,7 +2,10 @@
 all-reduces are identities without torch.distributed), for rocprofv3 kernel stats
 of the sharded WTA kernels and the replicated side kernels.
 
-    python tools/shard_frame_bench.py [--world 4] [--rank 1] [--reps 5]
+    python tools/shard_frame_bench.py [--world 4] [--rank 1] [--reps 5] [--variants 0,3145728 --rounds 2]
+
+--variants: asw_tune_set(ASW_TUNE_PASS_VARIANT) values, timed in turn (interleaved over
+--rounds) on one matcher, one JSON line each.
 """
 import argparse
 import json
@@ -27,24 +30,32 @@ def main():
                     help="c4: 1920x1080 D256 T35; c5: 3840x2160 D512 T51 (native LR)")
     ap.add_argument("--support-index", default="", choices=["", "1", "v"],
                     help="index-form supports (asw_aggregate_pass_index): both directions, or V only (A/B)")
+    ap.add_argument("--variants", default="0")
+    ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
+    from stereo_matchin_amd import _lib
+    lib = _lib.lib()
     dev = torch.device("cuda:0")
     W, H, D, T, r = (1920, 1080, 256, 35, 7) if a.workload == "c4" else (3840, 2160, 512, 51, 7)
     Lh, Rh, _ = make_pair(W, H, D, 0)
     L, R = torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev)
     p = make_params(W, H, ndisp=D, taps=T, iters=r, lr_check=1, lr_mode=1 if D > 256 else 0)
     m = ShardedStereoMatcher(p, a.rank, a.world, dev, support_index={"": None, "1": True, "v": "v"}[a.support_index])
-    m.match(L, R)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.reps):
-        m.match(L, R)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / a.reps
-    print(json.dumps({"workload": a.workload, "world": a.world, "rank": a.rank, "planes": m.p.d_stop - m.p.d_begin,
-                      "support_index": {"v": m.matcher.vidx, "h": m.matcher.hidx},
-                      "ms_per_shard_frame_no_collective": round(ms, 3)}))
-
+    for _ in range(a.rounds):
+        for v in [int(x) for x in a.variants.split(",")]:
+            old = lib.asw_tune_set(1, v)
+            m.match(L, R)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.reps):
+                m.match(L, R)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / a.reps
+            lib.asw_tune_set(1, old)
+            print(json.dumps({"workload": a.workload, "world": a.world, "rank": a.rank,
+                              "planes": m.p.d_stop - m.p.d_begin, "variant": v,
+                              "support_index": {"v": m.matcher.vidx, "h": m.matcher.hidx},
+                              "ms_per_shard_frame_no_collective": round(ms, 3)}), flush=True)
 
 if __name__ == "__main__":
     main()
