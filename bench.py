@@ -26,10 +26,12 @@ k+1 aggregates in a second set of volumes (distributed.PipelinedMatcher), so the
 exchange is hidden behind the next frame's passes; every frame's work is inside the
 timed region (the side stream is joined before the closing synchronize).
 
-Rank 0 prints ONE JSON line.  ``roofline`` is the dominant kernel: the V
-aggregation pass with cached denominators (k_vpass10, DEN_READ: r-1 of the 2r
-launches per frame, the largest share of the frame; the H pass is reported beside
-it).  achieved = algorithmic bytes per launch ``8*n*S + 8*T*S`` (read + write the
+Rank 0 prints ONE JSON line.  ``roofline`` is the dominant kernel: the
+(direction, den mode) of aggregation pass with the most pass time per frame — on
+one GPU the V pass with cached denominators (k_vpass10, DEN_READ: r-1 of the 2r
+launches), on an 8-way C4 shard the den-none 32-plane pass (k_hpass32 / k_vpass32)
+— named by asw_pass_kernel right after the timed region, every other kind reported
+beside it.  achieved = algorithmic bytes per launch ``8*n*S + 8*T*S`` (read + write the
 n local cost planes, read both support arrays of the direction) over
 the launch's average duration from HIP events recorded on the stream the passes
 run on, inside the timed region.  ``traffic`` = that kernel's HBM bytes per
@@ -167,17 +169,42 @@ def _ranges(cpus):
     return ",".join(out)
 
 
-def ran_kernel(direction):
-    """The instantiation the library last launched for (direction, DEN_READ) in this process
+DM_NAMES = {0: "DM_NONE", 1: "DM_WRITE", 2: "DM_READ"}
+DM_LABEL = {0: "den-none", 1: "den-write", 2: "den-read"}
+
+
+def ran_kernel(direction, den_mode):
+    """The instantiation the library last launched for (direction, den_mode) in this process
     (asw_pass_kernel, e.g. "k_hpass11<T=35,NKW=4,DM=2,nt>"), and its traffic.json keys:
-    "<kernel><T=..,DM_READ>" then the older "<kernel><DM_READ>"."""
-    from stereo_matchin_amd import _lib
+    "<kernel><T=..,DM_x>" then the older "<kernel><DM_x>".  Call it right after the timed
+    region: a later run (frame_groups) launches other instantiations."""
     from stereo_matchin_amd import kernels as K
-    full = K.pass_kernel(direction, _lib.DEN_READ) or "unknown<>"
+    full = K.pass_kernel(direction, den_mode) or "unknown<>"
     base = full.split("<")[0]
     taps = [a for a in full[len(base) + 1:-1].split(",") if a.startswith("T=")]
-    keys = ([f"{base}<{taps[0]},DM_READ>"] if taps else []) + [f"{base}<DM_READ>"]
+    dm = DM_NAMES[den_mode]
+    keys = ([f"{base}<{taps[0]},{dm}>"] if taps else []) + [f"{base}<{dm}>"]
     return full, keys
+
+
+def base_matcher(m):
+    """The StereoMatcher that runs the passes of a (Pipelined / Sharded) matcher."""
+    from stereo_matchin_amd.distributed import PipelinedMatcher, ShardedStereoMatcher
+    if isinstance(m, PipelinedMatcher):
+        m = m.sets[0]
+    if isinstance(m, ShardedStereoMatcher):
+        m = m.matcher
+    return m
+
+
+def pass_den_mode(bm, name, it):
+    """Den mode of iteration `it`'s pass `name` ("v"/"h") as StereoMatcher.aggregate runs
+    it: none without a denominator volume (a 32-plane shard), else write then read."""
+    from stereo_matchin_amd import _lib
+    den = bm.den_v if name == "v" else bm.den_h
+    if den is None:
+        return _lib.DEN_NONE
+    return _lib.DEN_WRITE if it == 0 else _lib.DEN_READ
 
 
 def load_traffic(path, workload, n_gpus, keys):
@@ -325,9 +352,15 @@ def main():
     elapsed = time.perf_counter() - t0
     torch.cuda.synchronize()
 
-    # per-launch aggregation-pass durations from the events around each pass:
-    # iteration 0 writes the cached denominators (DEN_WRITE), iterations 1..r-1 read them
-    v_rd, h_rd, v_wr, h_wr, frame_ms, refine_ms = [], [], [], [], [], []
+    # the instantiations the timed frames ran, per (direction, den mode), queried now:
+    # the frame_groups run below launches other ones
+    from stereo_matchin_amd import _lib
+    ran = {(d, dm): ran_kernel(d, dm) for d in (0, 1) for dm in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ)}
+    # per-launch aggregation-pass durations from the events around each pass, classified
+    # by the den mode the pass ran: with cached denominators iteration 0 writes them
+    # (DEN_WRITE) and iterations 1..r-1 read them; a 32-plane shard runs DEN_NONE throughout
+    per_kind = {}  # ("v"|"h", den mode) -> [ms per launch]
+    frame_ms, refine_ms = [], []
     if frame:
         for t in spans:
             frame_ms.append(t["total"] + t["refine"])
@@ -338,10 +371,13 @@ def main():
             with FrameContext(p, devices=[local]) as eager:
                 per_pass = [eager.match(*pairs_h[0])["timings"] for _ in range(3)]
         for t in per_pass:
-            # asw_timings keeps the per-direction mean over the r passes of a frame
-            v_rd.append(t["v_pass_mean"])
-            h_rd.append(t["h_pass_mean"])
+            # asw_timings keeps the per-direction mean over the r passes of a frame (the
+            # context caches denominators for r >= 2: r - 1 of the r are den-read)
+            dm_f = _lib.DEN_READ if iters >= 2 else _lib.DEN_NONE
+            per_kind.setdefault(("v", dm_f), []).append(t["v_pass_mean"])
+            per_kind.setdefault(("h", dm_f), []).append(t["h_pass_mean"])
     else:
+        bm = base_matcher(m)
         for ev in evs:
             prev = dict(ev)["support"]
             it = {"v": 0, "h": 0}
@@ -349,9 +385,7 @@ def main():
                 if name == "refine":
                     refine_ms.append(dict(ev)["consistency"].elapsed_time(e))
                 if name in ("v", "h"):
-                    ms = prev.elapsed_time(e)
-                    first = it[name] == 0
-                    {("v", True): v_wr, ("v", False): v_rd, ("h", True): h_wr, ("h", False): h_rd}[(name, first)].append(ms)
+                    per_kind.setdefault((name, pass_den_mode(bm, name, it[name])), []).append(prev.elapsed_time(e))
                     it[name] += 1
                     prev = e
             frame_ms.append(ev[0][1].elapsed_time(ev[-1][1]))
@@ -412,13 +446,21 @@ def main():
                         "note": f"{world // g2} concurrent frames, each d-sharded over {g2} GPUs "
                                 "(the most maps/s on N GPUs; not the headline layout)"}
         del m2
-    mean = lambda xs: float(np.mean(xs)) if xs else float("nan")  # noqa: E731
-    all_pass = v_rd + h_rd + v_wr + h_wr
-    stats = torch.tensor([elapsed, mean(v_rd), mean(h_rd), mean(v_wr), mean(h_wr), mean(all_pass),
-                          float(np.sum(frame_ms))], dtype=torch.float64, device=dev)
+    # max over ranks of every per-kind mean (absent kinds: -1) and of the launches per frame
+    kinds = [(n, dm) for n in ("v", "h") for dm in (_lib.DEN_READ, _lib.DEN_WRITE, _lib.DEN_NONE)]
+    nframes = max(len(frame_ms), 1) if not frame else max(len(per_pass), 1)
+    all_pass = [x for xs in per_kind.values() for x in xs]
+    vals = [elapsed, float(np.mean(all_pass)) if all_pass else -1.0, float(np.sum(frame_ms))]
+    for k in kinds:
+        xs = per_kind.get(k, [])
+        vals += [float(np.mean(xs)) if xs else -1.0, len(xs) / nframes]
+    stats = torch.tensor(vals, dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    elapsed, v_avg, h_avg, vw_avg, hw_avg, pass_avg, span_sum = stats.tolist()
+    vals = stats.tolist()
+    elapsed, pass_avg, span_sum = vals[:3]
+    kind_ms = {k: vals[3 + 2 * i] for i, k in enumerate(kinds) if vals[3 + 2 * i] >= 0}
+    kind_n = {k: vals[4 + 2 * i] for i, k in enumerate(kinds) if vals[3 + 2 * i] >= 0}
 
     if rank == 0:
         S = W * H
@@ -426,9 +468,13 @@ def main():
         gbs = lambda ms: bytes_per_pass / (ms * 1e-3) / 1e9  # noqa: E731
         n_maps = groups * args.steps * batch
         maps_per_s = n_maps / (span_sum / 1e3) if frame else n_maps / elapsed
-        dom = "v" if (v_avg >= h_avg or h_avg != h_avg) else "h"
-        dom_ms = v_avg if dom == "v" else h_avg
-        kname, tkeys = ran_kernel(0 if dom == "v" else 1)
+        # the dominant kernel: the (direction, den mode) with the most pass time per frame
+        dom = max(kind_ms, key=lambda k: kind_ms[k] * kind_n[k]) if kind_ms else ("v", _lib.DEN_READ)
+        dom_ms = kind_ms.get(dom, float("nan"))
+        kname, tkeys = ran[(0 if dom[0] == "v" else 1, dom[1])]
+        opt = lambda k: round(kind_ms[k], 4) if k in kind_ms else None  # noqa: E731
+        optf = lambda k: round(gbs(kind_ms[k]) / HBM_PEAK_GBS, 4) if k in kind_ms else None  # noqa: E731
+        in_frame_none = ("v", _lib.DEN_NONE) in kind_ms or ("h", _lib.DEN_NONE) in kind_ms
         out = {
             "metric": METRIC,
             "value": round(maps_per_s, 4),
@@ -453,19 +499,29 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(gbs(dom_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs(dom_ms) / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(args.traffic, args.workload, world, tkeys),
-                         "kernel": f"{kname}: {'V' if dom == 'v' else 'H'} aggregation pass reading cached "
-                                   f"denominators ({max(iters - 1, 0)} of the {2 * iters} launches per frame)",
+                         "kernel": f"{kname}: {'V' if dom[0] == 'v' else 'H'} aggregation pass, "
+                                   f"{DM_LABEL[dom[1]]} ({round(kind_n.get(dom, 0))} of the {2 * iters} "
+                                   f"launches per frame)",
                          "bytes_per_launch": bytes_per_pass, "avg_launch_ms": round(dom_ms, 4),
-                         "v_read_ms": round(v_avg, 4), "v_read_frac": round(gbs(v_avg) / HBM_PEAK_GBS, 4),
-                         "h_read_ms": round(h_avg, 4), "h_read_frac": round(gbs(h_avg) / HBM_PEAK_GBS, 4),
-                         "v_write_ms": round(vw_avg, 4), "h_write_ms": round(hw_avg, 4),
-                         "v_none_ms": round(float(np.median(v_none)), 4) if v_none else None,
-                         "v_none_frac": round(gbs(float(np.median(v_none))) / HBM_PEAK_GBS, 4) if v_none else None,
-                         "h_none_ms": round(float(np.median(h_none)), 4) if h_none else None,
-                         "h_none_frac": round(gbs(float(np.median(h_none))) / HBM_PEAK_GBS, 4) if h_none else None,
-                         "den_modes": "the frame ships cached denominators (den-read) for r >= 2: den-none "
-                                      "(v/h_none, 3 VALU per voxel-tap instead of 2, 2.1 GB less traffic) is "
-                                      "timed beside it outside the timed region",
+                         "v_read_ms": opt(("v", _lib.DEN_READ)), "v_read_frac": optf(("v", _lib.DEN_READ)),
+                         "h_read_ms": opt(("h", _lib.DEN_READ)), "h_read_frac": optf(("h", _lib.DEN_READ)),
+                         "v_write_ms": opt(("v", _lib.DEN_WRITE)), "h_write_ms": opt(("h", _lib.DEN_WRITE)),
+                         "v_none_ms": opt(("v", _lib.DEN_NONE)) if in_frame_none else
+                         (round(float(np.median(v_none)), 4) if v_none else None),
+                         "v_none_frac": optf(("v", _lib.DEN_NONE)) if in_frame_none else
+                         (round(gbs(float(np.median(v_none))) / HBM_PEAK_GBS, 4) if v_none else None),
+                         "h_none_ms": opt(("h", _lib.DEN_NONE)) if in_frame_none else
+                         (round(float(np.median(h_none)), 4) if h_none else None),
+                         "h_none_frac": optf(("h", _lib.DEN_NONE)) if in_frame_none else
+                         (round(gbs(float(np.median(h_none))) / HBM_PEAK_GBS, 4) if h_none else None),
+                         "kernels_ran": {f"{'VH'[d]} {DM_LABEL[dm]}": ran[(d, dm)][0]
+                                         for (n, dm) in kind_ms for d in [0 if n == "v" else 1]},
+                         "den_modes": ("the frame's passes run den-none (a 32-plane shard keeps no denominator "
+                                       "volumes): v/h_none are those passes, timed inside the timed region"
+                                       if in_frame_none else
+                                       "the frame ships cached denominators (den-read) for r >= 2: den-none "
+                                       "(v/h_none, 3 VALU per voxel-tap instead of 2, 2.1 GB less traffic) is "
+                                       "timed beside it outside the timed region"),
                          "all_pass_mean_ms": round(pass_avg, 4),
                          "all_pass_frac": round(gbs(pass_avg) / HBM_PEAK_GBS, 4),
                          "timing": "frame API: asw_timings per-direction means over all r passes" if frame else

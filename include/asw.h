@@ -65,7 +65,21 @@ typedef struct asw_params {
     int lr_check;        /* run the left-right consistency stage                */
     int lr_mode;         /* ASW_LR_*                                             */
     int d_begin, d_end;  /* disparity shard owned by this context [begin, end)  */
+    int flags;           /* ASW_FLAG_*: frame-API context options (0 = the default forms) */
 } asw_params;
+
+/* asw_params.flags: forms a context (asw_create*) allocates and runs instead of the
+ * default ones.  Every form is bit-identical to the default; each was measured slower
+ * on MI355X where it is built and is kept opt-in.  A flag whose form is not
+ * built for the shape is ignored (the default form runs).  The stage API ignores flags;
+ * asw_params_check rejects unknown bits. */
+#define ASW_FLAG_FUSE_RAW 0x1        /* asw_Aggr fused into the first V pass (asw_aggregate_pass_raw)     */
+#define ASW_FLAG_SUPPORT_INDEX 0x2   /* 32-plane shards: index-form supports, both directions            */
+#define ASW_FLAG_SUPPORT_INDEX_V 0x4 /* 32-plane shards: index-form supports, the V passes only          */
+#define ASW_FLAG_OTF_H 0x8           /* right H weights on the fly (asw_aggregate_pass_otf), no whr array */
+#define ASW_FLAG_SHARD_DEN_H 0x10    /* 32-plane shards: cache the H denominators (den-write / den-read) */
+#define ASW_FLAG_COMM_LOCAL 0x20     /* asw_create_multi: the device-local exchange even for distinct ids */
+#define ASW_FLAG_ALL 0x3F
 
 void asw_params_default(asw_params *p);
 int asw_params_check(const asw_params *p);
@@ -75,8 +89,9 @@ int asw_last_hip_error(void); /* hipError_t of the last ASW_E_HIP */
  * (asw_outputs, asw_timings) grow between revisions: a host must check
  * asw_abi_version() == ASW_ABI_VERSION before calling asw_match / asw_match_batch,
  * or the library writes past a struct of an older layout.
- *   1: round 1;  2: asw_outputs.disp16 / lr16, asw_timings.exchange. */
-#define ASW_ABI_VERSION 2
+ *   1: round 1;  2: asw_outputs.disp16 / lr16, asw_timings.exchange;
+ *   3: asw_params.flags (the context options that were environment variables). */
+#define ASW_ABI_VERSION 3
 int asw_abi_version(void);
 
 /* layout helpers */
@@ -164,6 +179,8 @@ int asw_pass_otf_supported(const asw_params *p, int dir);
  * counts, not a 32-plane shard: ASW_E_UNSUPPORTED otherwise. */
 int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
                            const uint8_t *right_rgba, float *cout, float *den, int den_mode, void *stream);
+/* 1 when asw_aggregate_pass_raw is built for p (and p->iters >= 1), else 0 */
+int asw_pass_raw_supported(const asw_params *p);
 
 /* ---- support arrays in INDEX form (the support stream of a d-shard) ----
  * A pass reads its direction's two support arrays, 8*T*S bytes, whatever its plane

@@ -33,7 +33,7 @@ DISP16_INVALID = 0xFFFF
 COMM_ID_BYTES = 128
 # the asw_outputs / asw_timings layouts mirrored below (ASW_ABI_VERSION of include/asw.h):
 # a library of another revision would write past them, so _load() refuses it
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 DIR_V = 0
 DIR_H = 1
@@ -42,6 +42,13 @@ COLOR_RGB = 0
 COLOR_LAB = 1
 LR_U8 = 0
 LR_NATIVE = 1
+# asw_params.flags (ASW_FLAG_*): frame-API context options, the opt-in forms
+FLAG_FUSE_RAW = 0x1
+FLAG_SUPPORT_INDEX = 0x2
+FLAG_SUPPORT_INDEX_V = 0x4
+FLAG_OTF_H = 0x8
+FLAG_SHARD_DEN_H = 0x10
+FLAG_COMM_LOCAL = 0x20
 
 
 class AswLibraryError(RuntimeError):
@@ -67,6 +74,7 @@ class AswParams(ctypes.Structure):
         ("color_space", ctypes.c_int), ("tad_tau", ctypes.c_float),
         ("lr_check", ctypes.c_int), ("lr_mode", ctypes.c_int),
         ("d_begin", ctypes.c_int), ("d_end", ctypes.c_int),
+        ("flags", ctypes.c_int),
     ]
 
     def copy(self) -> "AswParams":
@@ -138,6 +146,7 @@ SIGNATURES = {
     "asw_aggregate_pass_raw": (I, [PP, P, P, P, P, P, P, I, P]),
     "asw_aggregate_pass_otf": (I, [PP, I, P, P, P, P, P, P, I, P]),
     "asw_pass_otf_supported": (I, [PP, I]),
+    "asw_pass_raw_supported": (I, [PP]),
     "asw_support_index_bytes": (ctypes.c_size_t, [PP]),
     "asw_support_all_fmt": (I, [PP, P, P, P, P, P, P, P, I, P]),
     "asw_aggregate_pass_index": (I, [PP, I, P, P, P, P, P, P, I, P]),

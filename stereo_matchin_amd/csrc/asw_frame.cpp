@@ -263,17 +263,16 @@ int alloc_shard(Shard &s, bool sharded) {
     // asw_Aggr fused into the first V pass (k_vpass10_raw): the raw-cost volume is never
     // written nor read, bit-identical, but measured slower at C4 (2.40 ms against 0.37 +
     // 1.78 ms; frame 23.40 either way, profiles/r04/fused_raw_r10d.log), so the two
-    // kernels stay the default; ASW_FUSE_RAW=1 selects the fused pass
-    const char *fuse_env = std::getenv("ASW_FUSE_RAW");
-    s.fuse = fuse_env && fuse_env[0] == '1' && p->iters >= 1 && asw::ring_taps(p->taps) && asw_disp_pitch(p) != 32;
+    // kernels stay the default; ASW_FLAG_FUSE_RAW selects the fused pass
+    s.fuse = (p->flags & ASW_FLAG_FUSE_RAW) && asw_pass_raw_supported(p);
     // a 32-plane shard can read its supports in index form (uint16 LUT
     // indices, half the bytes of the replicated support stream; asw_aggregate_pass_index),
     // bit-identical but measured slower: its passes are LDS-bound and the LUT reads cost
     // more LDS cycles than the bytes save (C4 / 8: V 0.351 against 0.265 ms, H 0.68 against
     // 0.36; shard frame 7.10 against 5.13 ms, profiles/r04/index_form_r10b.log).  Opt-in:
-    // ASW_SUPPORT_INDEX=1 (both directions) or =v (the V passes only)
-    const char *idx_env = std::getenv("ASW_SUPPORT_INDEX");
-    const bool idx_on = idx_env && (idx_env[0] == '1' || idx_env[0] == 'v'), v_only = idx_env && idx_env[0] == 'v';
+    // ASW_FLAG_SUPPORT_INDEX (both directions) or ASW_FLAG_SUPPORT_INDEX_V (the V passes only)
+    const bool idx_on = p->flags & (ASW_FLAG_SUPPORT_INDEX | ASW_FLAG_SUPPORT_INDEX_V);
+    const bool v_only = !(p->flags & ASW_FLAG_SUPPORT_INDEX);
     s.vidx = idx_on && asw_pass_index_supported(p, ASW_DIR_V, ASW_DEN_NONE) != 0;
     s.hidx = idx_on && !v_only && s.vidx && asw_pass_index_supported(p, ASW_DIR_H, ASW_DEN_READ) != 0;
     const size_t vbytes = s.vidx ? asw_support_index_bytes(p) : asw_support_bytes(p);
@@ -283,20 +282,18 @@ int alloc_shard(Shard &s, bool sharded) {
     ASWCHK(dev_alloc(&s.whl, hbytes));
     // the right H weights can be computed inside the H passes
     // (asw_aggregate_pass_otf, the array then never built): bit-identical but measured
-    // slower at C4 (H den-read 2.30 against 1.42 ms), so only on request (ASW_OTF=1)
-    const char *otf_env = std::getenv("ASW_OTF");
-    s.otf = otf_env && otf_env[0] == '1' && asw_pass_otf_supported(p, ASW_DIR_H) != 0;
+    // slower at C4 (H den-read 2.30 against 1.42 ms), so only on request (ASW_FLAG_OTF_H)
+    s.otf = (p->flags & ASW_FLAG_OTF_H) && asw_pass_otf_supported(p, ASW_DIR_H) != 0;
     if (!s.otf) ASWCHK(dev_alloc(&s.whr, hbytes));
     ASWCHK(dev_alloc(&s.c0, asw_cost_bytes(p)));
     ASWCHK(dev_alloc(&s.c1, asw_cost_bytes(p)));
     if (p->iters >= 2) {  // the den of a direction is written by its first pass and read by the r-1 others
         // (a 32-plane shard's passes recompute it: at C4 / 8 k_vpass32 den-none 0.24 against
         // den-read 0.28 ms, k_hpass32 0.30-0.33 against 0.36, profiles/r04/h32_variants_r11d.log;
-        // ASW_SHARD_DEN_H=1 keeps the H pass reading it)
-        const char *denh_env = std::getenv("ASW_SHARD_DEN_H");
+        // ASW_FLAG_SHARD_DEN_H keeps the H pass reading it)
         const bool p32 = asw_disp_pitch(p) == 32;
         if (!p32) ASWCHK(dev_alloc(&s.den_v, asw_cost_bytes(p)));
-        if (!p32 || (denh_env && denh_env[0] == '1')) ASWCHK(dev_alloc(&s.den_h, asw_cost_bytes(p)));
+        if (!p32 || (p->flags & ASW_FLAG_SHARD_DEN_H)) ASWCHK(dev_alloc(&s.den_h, asw_cost_bytes(p)));
     }
     if (sharded) {
         ASWCHK(dev_alloc(&s.key, S * 8));
@@ -775,8 +772,7 @@ int asw_create_multi(const asw_params *p, const int *hip_device_ids, int n_devic
     for (int i = 0; i < n_devices; ++i)
         for (int j = 0; j < i; ++j)
             if (hip_device_ids[i] == hip_device_ids[j]) comm = COMM_LOCAL;  // RCCL needs one rank per device
-    const char *force = std::getenv("ASW_COMM");
-    if (n_devices > 1 && force && std::strcmp(force, "local") == 0) comm = COMM_LOCAL;
+    if (n_devices > 1 && p && (p->flags & ASW_FLAG_COMM_LOCAL)) comm = COMM_LOCAL;
     return create_ctx(p, hip_device_ids, n_devices, 0, n_devices, comm, nullptr, out);
 }
 

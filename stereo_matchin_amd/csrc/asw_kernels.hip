@@ -651,6 +651,7 @@ extern "C" {
 
 // 2: asw_outputs gained disp16 / lr16 and asw_timings gained exchange (round 2);
 // asw_create rejects shapes the pass kernels cannot address (ASW_E_UNSUPPORTED)
+// 3: asw_params.flags (round 5)
 int asw_abi_version(void) { return ASW_ABI_VERSION; }
 
 // 0: lane-per-pixel scans (default), 1: wave per pixel, 2: asw_WTA by the row sweep
@@ -693,6 +694,7 @@ void asw_params_default(asw_params *p) {
     p->lr_mode = ASW_LR_U8;
     p->d_begin = 0;
     p->d_end = -1;  // -1: = ndisp
+    p->flags = 0;
 }
 
 static inline int d_end_of(const asw_params *p) { return p->d_end < 0 ? p->ndisp : p->d_end; }
@@ -705,6 +707,7 @@ int asw_params_check(const asw_params *p) {
     if (p->color_space != ASW_COLOR_RGB && p->color_space != ASW_COLOR_LAB) return ASW_E_INVALID;
     if (p->lr_mode != ASW_LR_U8 && p->lr_mode != ASW_LR_NATIVE) return ASW_E_INVALID;
     if ((long long)p->width * p->height > (1LL << 31) / 64) return ASW_E_INVALID;
+    if (p->flags & ~ASW_FLAG_ALL) return ASW_E_INVALID;
     return ASW_OK;
 }
 
@@ -907,6 +910,12 @@ int asw_pass_otf_supported(const asw_params *p, int dir) {
     // (a 32-plane shard's half-wave H pass reads the materialised array)
     return dir == ASW_DIR_H && p->color_space == ASW_COLOR_RGB && asw::ring_taps(p->taps) && asw_disp_pitch(p) != 32
                ? 1 : 0;
+}
+
+int asw_pass_raw_supported(const asw_params *p) {
+    if (!p || asw_params_check(p) != ASW_OK) return 0;
+    // ring kernels only (in a make DEV=1 library: its one tap count), not a 32-plane shard
+    return p->iters >= 1 && asw::ring_taps(p->taps) && asw_disp_pitch(p) != 32 ? 1 : 0;
 }
 
 int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,

@@ -255,12 +255,10 @@ def asw_vCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None,
     return _pass(p, DIR_V, supp_left, supp_right, cost_in, out, den, den_mode)
 
 
-RING_TAPS = (3, 5, 7, 9, 15, 33, 35, 51)  # tap counts with ring kernels (asw_aggregate.hip ring_taps)
-
-
 def raw_fused_supported(p: AswParams) -> bool:
-    """asw_aggregate_pass_raw is built for p: ring tap counts, not a 32-plane shard."""
-    return p.iters >= 1 and p.taps in RING_TAPS and cost_shape(p)[2] != 32
+    """asw_pass_raw_supported: asw_aggregate_pass_raw is built for p (ring tap counts of
+    this library build, not a 32-plane shard, r >= 1)."""
+    return bool(_lib.lib().asw_pass_raw_supported(ctypes.byref(p)))
 
 
 def asw_vCostAggregation_raw(p: AswParams, supp_left, supp_right, left, right, out=None, den=None,

@@ -13,7 +13,6 @@ CLI path.
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -58,9 +57,9 @@ class StereoMatcher:
         # asw_Aggr fused into the first V pass (k_vpass10_raw, asw_aggregate_pass_raw): the
         # raw-cost volume is never written nor read; bit-identical, measured slower at C4
         # (2.40 ms against 0.37 + 1.78, profiles/r04/fused_raw_r10d.log).  Default (None):
-        # off unless ASW_FUSE_RAW=1 (where built: ring tap counts, not a 32-plane shard)
+        # params.flags & ASW_FLAG_FUSE_RAW (where built: ring tap counts, not a 32-plane shard)
         if fuse_raw is None:
-            fuse_raw = os.environ.get("ASW_FUSE_RAW", "0") == "1"
+            fuse_raw = bool(params.flags & _lib.FLAG_FUSE_RAW)
         self.fuse_raw = bool(fuse_raw) and K.raw_fused_supported(self.p)
         self.device = torch.device(device)
         dev = self.device
@@ -69,7 +68,9 @@ class StereoMatcher:
         # (asw_aggregate_pass_otf), so whr is never built.  Off by default: bit-identical
         # but measured slower (C4 H den-read 2.30 against 1.42 ms: the refill pipeline's
         # registers cost the pass its latency cover; DESIGN.md §On-the-fly supports)
-        self.otf = False if otf is None else (otf and K.otf_supported(self.p))
+        if otf is None:
+            otf = bool(params.flags & _lib.FLAG_OTF_H)
+        self.otf = bool(otf) and K.otf_supported(self.p)
         # otf: a matcher-owned copy of the right image (the H passes read it after
         # raw_and_support returns; the caller's buffer may be reused by then)
         self.right = torch.empty((self.p.height, self.p.width, 4), dtype=torch.uint8, device=dev) \
@@ -80,7 +81,10 @@ class StereoMatcher:
         # passes only.  Bit-identical, measured slower (C4 / 8: V 0.351 against 0.265 ms,
         # H 0.68 against 0.36; the passes are LDS-bound and the LUT reads cost more LDS
         # cycles than the halved bytes save; DESIGN.md §Support stream)
-        want = False if support_index is None else support_index
+        want = support_index
+        if want is None:  # the context flags (ASW_FLAG_SUPPORT_INDEX / _V), as asw_create reads them
+            want = True if params.flags & _lib.FLAG_SUPPORT_INDEX else \
+                "v" if params.flags & _lib.FLAG_SUPPORT_INDEX_V else False
         self.vidx = bool(want) and K.index_supported(self.p, DIR_V, _lib.DEN_NONE)
         self.hidx = self.vidx and want != "v" and not self.otf and K.index_supported(self.p, DIR_H, _lib.DEN_READ)
         new_v = K.new_support_index if self.vidx else K.new_support
@@ -95,12 +99,12 @@ class StereoMatcher:
         if den_cache and self.p.iters >= 2:
             # a 32-plane shard's passes recompute den (C4 / 8: k_vpass32 den-none 0.24
             # against den-read 0.28 ms, k_hpass32 0.30-0.33 against 0.36,
-            # profiles/r04/h32_variants_r11d.log; ASW_SHARD_DEN_H=1 keeps the H pass
+            # profiles/r04/h32_variants_r11d.log; ASW_FLAG_SHARD_DEN_H keeps the H pass
             # reading it; asw_frame.cpp the same)
             p32 = K.cost_shape(self.p)[2] == 32
             if not p32:
                 self.den_v = K.new_cost(self.p, dev)
-            if not p32 or os.environ.get("ASW_SHARD_DEN_H", "0") == "1":
+            if not p32 or params.flags & _lib.FLAG_SHARD_DEN_H:
                 self.den_h = K.new_cost(self.p, dev)
 
     # -- stages ---------------------------------------------------------------

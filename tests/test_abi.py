@@ -27,7 +27,7 @@ def test_every_header_symbol_is_exported(L):
 
 def test_abi_version(L):
     import re
-    assert L.lib().asw_abi_version() == 2
+    assert L.lib().asw_abi_version() == 3
     # the binding's mirrored struct layouts are the header's revision (_load refuses others)
     hdr = open(os.path.join(ROOT, "include", "asw.h")).read()
     assert int(re.search(r"#define ASW_ABI_VERSION (\d+)", hdr).group(1)) == L.ABI_VERSION
@@ -189,3 +189,38 @@ def test_pass_otf_support_and_errors(L):
         assert lib.asw_aggregate_pass_otf(ctypes.byref(pp), d, x, x, x, x, y, None, L.DEN_NONE, None) == \
             L.ASW_E_UNSUPPORTED
     assert lib.asw_aggregate_pass_otf(ctypes.byref(p), 1, None, x, x, x, y, None, L.DEN_NONE, None) == L.ASW_E_INVALID
+
+
+def test_params_flags(L):
+    """asw_params.flags (ABI 3): the opt-in forms are context options, not environment
+    variables; unknown bits are rejected."""
+    p = L.default_params(32, 32)
+    assert p.flags == 0
+    for f in (L.FLAG_FUSE_RAW, L.FLAG_SUPPORT_INDEX, L.FLAG_SUPPORT_INDEX_V, L.FLAG_OTF_H, L.FLAG_SHARD_DEN_H,
+              L.FLAG_COMM_LOCAL):
+        p.flags = f
+        assert L.params_check(p) == L.ASW_OK
+    p.flags = 0x40
+    assert L.params_check(p) == L.ASW_E_INVALID
+    hdr = open(os.path.join(ROOT, "include", "asw.h")).read()
+    for name in ("FUSE_RAW", "SUPPORT_INDEX", "SUPPORT_INDEX_V", "OTF_H", "SHARD_DEN_H", "COMM_LOCAL"):
+        import re
+        v = int(re.search(rf"#define ASW_FLAG_{name} (0x[0-9A-Fa-f]+)", hdr).group(1), 16)
+        assert v == getattr(L, f"FLAG_{name}")
+    # the library reads no environment switch (the flags replaced them)
+    src = open(os.path.join(ROOT, "stereo_matchin_amd", "csrc", "asw_frame.cpp")).read()
+    assert "getenv" not in src
+
+
+def test_pass_raw_supported(L):
+    """asw_pass_raw_supported: the fused raw-cost first V pass is built for ring tap
+    counts of this library build, not for a 32-plane shard, and needs r >= 1."""
+    lib = L.lib()
+    p = L.default_params(64, 32, ndisp=64, taps=35)
+    assert lib.asw_pass_raw_supported(ctypes.byref(p)) == 1
+    assert lib.asw_pass_raw_supported(ctypes.byref(L.default_params(64, 32, ndisp=64, taps=11))) == 0
+    assert lib.asw_pass_raw_supported(ctypes.byref(L.default_params(64, 32, ndisp=64, taps=35, iters=0))) == 0
+    shard = L.default_params(64, 32, ndisp=256, taps=35, d_begin=32, d_end=64)
+    assert lib.asw_pass_raw_supported(ctypes.byref(shard)) == 0
+    from stereo_matchin_amd import kernels as K
+    assert K.raw_fused_supported(p) and not K.raw_fused_supported(shard)

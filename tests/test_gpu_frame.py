@@ -57,15 +57,16 @@ def test_multi_shard_local_equals_single(gpu, oracle, n):
 
 
 # C4's D = 256 over 8 shards of 32 planes (pitch 32: the half-wave passes), with float
-# supports (default) and index-form supports (ASW_SUPPORT_INDEX=1 / =v, read at create)
+# supports (default) and index-form supports (asw_params.flags ASW_FLAG_SUPPORT_INDEX /
+# ASW_FLAG_SUPPORT_INDEX_V, read at create)
 @pytest.mark.parametrize("index", ["", "1", "v"])
-def test_multi_shard_d256_eight_way(gpu, monkeypatch, index):
-    from stereo_matchin_amd import FrameContext
+def test_multi_shard_d256_eight_way(gpu, index):
+    from stereo_matchin_amd import FrameContext, _lib
     Lh, Rh = _pair(7, 96, 320, shift=40)
     p = _p(320, 96, 256, 35, 2)
     with FrameContext(p, devices=[0]) as one:
         ref = one.match(Lh, Rh)
-    monkeypatch.setenv("ASW_SUPPORT_INDEX", index)
+    p.flags = {"": 0, "1": _lib.FLAG_SUPPORT_INDEX, "v": _lib.FLAG_SUPPORT_INDEX_V}[index]
     with FrameContext(p, devices=[0] * 8) as fc:
         assert [e - b for b, e in fc.shards()] == [32] * 8
         got = fc.match(Lh, Rh)

@@ -110,8 +110,9 @@ def test_pass32_rejects_fused_raw_and_otf(gpu):
 # the C4 shard of the 8-way split: one rank's 32 planes of a 1920-column D256 T35
 # frame through the whole r = 7 pass sequence, on a full-width band of 215 rows (the
 # oracle's passes over all 1080 rows take minutes), against the oracle on that band
-def test_c4_shard_band_r7(gpu, oracle, monkeypatch):
+def test_c4_shard_band_r7(gpu, oracle):
     import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
     from stereo_matchin_amd.pipeline import StereoMatcher
     from stereo_matchin_amd.synthetic import make_pair
     W, H, D, T, r = 1920, 1080, 256, 35, 7
@@ -127,9 +128,9 @@ def test_c4_shard_band_r7(gpu, oracle, monkeypatch):
         cost = oracle.aggregate_pass(*sv, cost, T, 0, d0=d0, d1=d1, plane_base=d0)
         cost = oracle.aggregate_pass(*sh, cost, T, 1, d0=d0, d1=d1, plane_base=d0)
     # float supports (the default), index-form supports (opt-in), and
-    # float supports with the H denominators cached (ASW_SHARD_DEN_H=1)
+    # float supports with the H denominators cached (ASW_FLAG_SHARD_DEN_H)
     for index, denh in ((None, "0"), (True, "0"), (None, "1")):
-        monkeypatch.setenv("ASW_SHARD_DEN_H", denh)
+        p.flags = _lib.FLAG_SHARD_DEN_H if denh == "1" else 0
         m = StereoMatcher(p, gpu, support_index=index)
         m.raw_and_support(_t(Lb, gpu), _t(Rb, gpu))
         got = plane_major(_np(m.aggregate()), d1 - d0)

@@ -11,6 +11,7 @@
 #   profpy:ARGS rocprofv3 --kernel-trace --stats of python3 ARGS (a tool script)
 #   pass        tools/pass_bench.py (den modes, default variant)
 #   pmc         rocprofv3 --pmc counter sets (one run each) over tools/pass_bench.py
+#   pmcpy:ARGS  the same counter sets over python3 ARGS (e.g. tools/shard_frame_bench.py+--world+8)
 #   calib       rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over tools/ubench/fetch_calib
 #   traffic     rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, over bench.py (C4 frame) -> $OUT/traffic
 #   cmd:STR     any other command (STR runs under bash with a 300 s limit)
@@ -75,6 +76,13 @@ for step in "$@"; do
                 i=$((i + 1))
                 run 300 "pmc_$TAG$i" rocprofv3 --pmc $set --output-format csv -d "$OUT/pmc/p$i" -o run -- \
                     python3 tools/pass_bench.py --reps 1 --den ${args:---variants 0}
+            done ;;
+        pmcpy)  # every counter set over any python script: pmcpy:tools/x.py+--arg+v -> $OUT/pmcpy/p<i>
+            i=0
+            for set in "${PMC_SETS[@]}"; do
+                i=$((i + 1))
+                run 300 "pmcpy_$TAG$i" rocprofv3 --pmc $set --output-format csv -d "$OUT/pmcpy/p$i" -o run -- \
+                    python3 $args
             done ;;
         calib)
             for c in FETCH_SIZE WRITE_SIZE; do
