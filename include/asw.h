@@ -79,7 +79,11 @@ typedef struct asw_params {
 #define ASW_FLAG_OTF_H 0x8           /* right H weights on the fly (asw_aggregate_pass_otf), no whr array */
 #define ASW_FLAG_SHARD_DEN_H 0x10    /* 32-plane shards: cache the H denominators (den-write / den-read) */
 #define ASW_FLAG_COMM_LOCAL 0x20     /* asw_create_multi: the device-local exchange even for distinct ids */
-#define ASW_FLAG_ALL 0x3F
+#define ASW_FLAG_RAW_F32 0x40        /* keep the float raw-cost volume (asw_raw_cost) where the uint16 one
+                                        (asw_raw_cost16 + asw_aggregate_pass_den16) is the default    */
+#define ASW_FLAG_OTF_V 0x80          /* 32-plane shards: both V weights on the fly (asw_aggregate_pass_otf_v),
+                                        no wvl / wvr arrays                                            */
+#define ASW_FLAG_ALL 0xFF
 
 void asw_params_default(asw_params *p);
 int asw_params_check(const asw_params *p);
@@ -90,7 +94,9 @@ int asw_last_hip_error(void); /* hipError_t of the last ASW_E_HIP */
  * asw_abi_version() == ASW_ABI_VERSION before calling asw_match / asw_match_batch,
  * or the library writes past a struct of an older layout.
  *   1: round 1;  2: asw_outputs.disp16 / lr16, asw_timings.exchange;
- *   3: asw_params.flags (the context options that were environment variables). */
+ *   3: asw_params.flags (the context options that were environment variables);
+ *      asw_raw_cost16 / asw_aggregate_pass_den16 (the uint16 raw-cost volume);
+ *      asw_aggregate_pass_otf_v (a shard's V weights on the fly). */
 #define ASW_ABI_VERSION 3
 int asw_abi_version(void);
 
@@ -111,6 +117,17 @@ size_t asw_lab_bytes(const asw_params *p);     /* H*W*16 (float4 per pixel) */
  * d = d_begin + k; padding lanes k >= d_end-d_begin are written 0. */
 int asw_raw_cost(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba, float *cost,
                  void *stream);
+/* The same costs as uint16 [H][W][Dp] (half the bytes): |dR|+|dG|+|dB| is an integer
+ * <= 765, so min(tad_tau, AD) is one too when tad_tau >= 765 or integral; other
+ * tad_tau (or tad_tau < 0): ASW_E_UNSUPPORTED.  asw_aggregate_pass_den16 reads it as the
+ * first V pass (main.cpp:494-500); the float values it converts are the ones
+ * asw_raw_cost writes, so every output is bit-identical.  asw_raw16_supported: 1 when
+ * both are built for p (that tad_tau, a ring tap count, iters >= 1), else 0. */
+int asw_raw_cost16(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba, uint16_t *cost,
+                   void *stream);
+int asw_aggregate_pass_den16(const asw_params *p, const float *wvl, const float *wvr, const uint16_t *cin16,
+                             float *cout, float *den, int den_mode, void *stream); /* V; den_mode NONE or WRITE */
+int asw_raw16_supported(const asw_params *p);
 
 /* support-weight table (the exp of K/asw_vsupport.cl:22-25 for every (|delta|, SAD)) */
 int asw_support_lut(const asw_params *p, float *lut, void *stream);
@@ -170,6 +187,18 @@ int asw_aggregate_pass_otf(const asw_params *p, int dir, const float *wl, const 
                            const float *lut, const float *cin, float *cout, float *den, int den_mode, void *stream);
 /* 1 when asw_aggregate_pass_otf supports (p, dir), else 0 */
 int asw_pass_otf_supported(const asw_params *p, int dir);
+
+/* The V pass (asw_vCostAggregation, K/asw_vcost_aggregation.cl:11-44) of a 32-plane
+ * shard (asw_disp_pitch 32) with BOTH support weights computed on the fly (SURVEY
+ * §8(f)3): each weight of the left and right pixels' vertical windows is computed from
+ * the device RGBA8 images and the support LUT as asw_support does (K/asw_vsupport.cl:
+ * 19-26), so the two asw_vSupport arrays (main.cpp:469-476) are never written nor read.
+ * Den mode NONE (a shard's V passes recompute den).  Bit-identical to
+ * asw_aggregate_pass_den(V, asw_support(V, left), asw_support(V, right), ..., NONE).
+ * RGB contexts, ring tap counts <= 35: see asw_pass_otf_v_supported. */
+int asw_aggregate_pass_otf_v(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba,
+                             const float *lut, const float *cin, float *cout, void *stream);
+int asw_pass_otf_v_supported(const asw_params *p);
 
 /* The first V pass of main.cpp:494-500 with asw_Aggr (main.cpp:463-466,
  * K/asw_aggr.cl:3-23) fused: each window element's raw AD/TAD cost is computed
@@ -311,8 +340,8 @@ int asw_refine(const asw_params *p, const asw_refine_params *rp, const uint8_t *
  * variants; returns the previous value, or ASW_E_INVALID for an unknown key.
  * Every variant computes bit-identical results. */
 #define ASW_TUNE_PASS_VARIANT 1
-#define ASW_TUNE_WTA_VARIANT 2 /* asw_wta: 0 lane-per-pixel scan (default), 1 wave-per-pixel reduction,
-                                  2 row sweep (Dp 64/128/256; the scan elsewhere) */
+#define ASW_TUNE_WTA_VARIANT 2 /* asw_wta: 0 lane-per-pixel scan (default), 2 row sweep (Dp 64/128/256; the
+                                  scan elsewhere); 1 (round 1's wave per pixel) is no longer built */
 int asw_tune_set(int key, int value);
 /* the kernel instantiation the most recent aggregation-pass launch of (dir, den_mode)
  * in this process ran, e.g. "k_vpass10<T=35,NW=16,DM=2,nt>" (NUL-terminated, at most

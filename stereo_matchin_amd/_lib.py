@@ -49,6 +49,8 @@ FLAG_SUPPORT_INDEX_V = 0x4
 FLAG_OTF_H = 0x8
 FLAG_SHARD_DEN_H = 0x10
 FLAG_COMM_LOCAL = 0x20
+FLAG_RAW_F32 = 0x40
+FLAG_OTF_V = 0x80
 
 
 class AswLibraryError(RuntimeError):
@@ -146,7 +148,12 @@ SIGNATURES = {
     "asw_aggregate_pass_raw": (I, [PP, P, P, P, P, P, P, I, P]),
     "asw_aggregate_pass_otf": (I, [PP, I, P, P, P, P, P, P, I, P]),
     "asw_pass_otf_supported": (I, [PP, I]),
+    "asw_aggregate_pass_otf_v": (I, [PP, P, P, P, P, P, P]),
+    "asw_pass_otf_v_supported": (I, [PP]),
     "asw_pass_raw_supported": (I, [PP]),
+    "asw_raw_cost16": (I, [PP, P, P, P, P]),
+    "asw_aggregate_pass_den16": (I, [PP, P, P, P, P, P, I, P]),
+    "asw_raw16_supported": (I, [PP]),
     "asw_support_index_bytes": (ctypes.c_size_t, [PP]),
     "asw_support_all_fmt": (I, [PP, P, P, P, P, P, P, P, I, P]),
     "asw_aggregate_pass_index": (I, [PP, I, P, P, P, P, P, P, I, P]),

@@ -19,6 +19,12 @@ int launch_pass_tm(const asw_params *p, int dir, const float *wl, const float *w
 template <int T, int DM>
 int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                      float *den, hipStream_t st);
+template <int T, int DM>
+int launch_pass32_c16_tm(const asw_params *p, const float *wl, const float *wr, const uint16_t *cin16, float *cout,
+                         float *den, hipStream_t st);
+template <int T>
+int launch_pass32_otf_v_t(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut,
+                          const float *cin, float *cout, hipStream_t st);
 template <int T>
 int launch_pass32_idx_tm(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
                          const float *cin, float *cout, float *den, int dm, hipStream_t st);
@@ -34,6 +40,11 @@ template <int T>
 int launch_pass_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                   float *den, int dm, hipStream_t st, const RawSrc *raw, const OtfSrc *otf) {
     if (asw_disp_pitch(p) == 32) {
+        if (raw && raw->cost16 && dir == ASW_DIR_V) {  // the first V pass over the uint16 raw costs
+            if (dm == 1) return launch_pass32_c16_tm<T, 1>(p, wl, wr, raw->cost16, cout, den, st);
+            if (dm == 0) return launch_pass32_c16_tm<T, 0>(p, wl, wr, raw->cost16, cout, den, st);
+            return ASW_E_INVALID;
+        }
         if (raw || otf) return ASW_E_UNSUPPORTED;  // the fused raw cost and on-the-fly weights: 64-lane passes only
         return launch_pass32_t<T>(p, dir, wl, wr, cin, cout, den, dm, st);
     }
@@ -85,6 +96,7 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
     if (dm != 0 && !den) return ASW_E_INVALID;
     if (const int s = pass_shape_check(p)) return s;
     if (otf && (dir != ASW_DIR_H || raw || !ring_taps(p->taps))) return ASW_E_UNSUPPORTED;
+    if (raw && (dir != ASW_DIR_V || (raw->cost16 && (dm == 2 || !ring_taps(p->taps))))) return ASW_E_UNSUPPORTED;
 #ifdef ASW_DEV_TAPS  // development build (make DEV=1): one ring-kernel tap count only
     if (p->taps == ASW_DEV_TAPS) return agg::launch_pass_t<ASW_DEV_TAPS>(p, dir, wl, wr, cin, cout, den, dm, st, raw, otf);
     if (raw) return ASW_E_UNSUPPORTED;
@@ -130,6 +142,36 @@ int launch_pass_index(const asw_params *p, int dir, const uint16_t *wl, const ui
 #define ASW_CASE(TT) \
     case TT:         \
         return agg::launch_pass32_idx_tm<TT>(p, dir, wl, wr, lut, cin, cout, den, dm, st);
+        ASW_CASE(3)
+        ASW_CASE(5)
+        ASW_CASE(7)
+        ASW_CASE(9)
+        ASW_CASE(15)
+        ASW_CASE(33)
+        ASW_CASE(35)
+#undef ASW_CASE
+        default: return ASW_E_UNSUPPORTED;
+    }
+}
+
+// the V pass of a 32-plane shard with both support weights on the fly
+// (asw_aggregate_pass_otf_v): RGB, ring tap counts <= 35, den mode NONE
+bool pass_otf_v_supported(const asw_params *p) {
+    return p->color_space == ASW_COLOR_RGB && asw_disp_pitch(p) == 32 && ring_taps(p->taps) && p->taps <= 35;
+}
+
+int launch_pass_otf_v(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut,
+                      const float *cin, float *cout, hipStream_t st) {
+    if (const int s = pass_shape_check(p)) return s;
+    if (!pass_otf_v_supported(p)) return ASW_E_UNSUPPORTED;
+#ifdef ASW_DEV_TAPS
+    if (p->taps == ASW_DEV_TAPS) return agg::launch_pass32_otf_v_t<ASW_DEV_TAPS>(p, left, right, lut, cin, cout, st);
+    return ASW_E_UNSUPPORTED;
+#endif
+    switch (p->taps) {
+#define ASW_CASE(TT) \
+    case TT:         \
+        return agg::launch_pass32_otf_v_t<TT>(p, left, right, lut, cin, cout, st);
         ASW_CASE(3)
         ASW_CASE(5)
         ASW_CASE(7)

@@ -37,6 +37,7 @@ __host__ __device__ inline int d_end_of_p(const asw_params *p) { return p->d_end
 // images of a V pass with the raw cost fused (asw_aggregate_pass_raw)
 struct RawSrc {
     const uint8_t *left, *right;
+    const uint16_t *cost16;  // (left = right = NULL) the raw costs as uint16 (asw_raw_cost16)
 };
 
 // right support weights of an H pass computed on the fly (asw_aggregate_pass_otf):

@@ -43,6 +43,8 @@ struct Shard {
     bool vidx = false; // wvl / wvr in index form (uint16 LUT indices; asw_aggregate_pass_index)
     bool hidx = false; // whl / whr likewise
     bool fuse = false; // asw_Aggr fused into the first V pass (asw_aggregate_pass_raw)
+    bool raw16 = false; // the raw costs as uint16 in c0 (asw_raw_cost16 + asw_aggregate_pass_den16)
+    bool otfv = false;  // a 32-plane shard's V passes compute both weights (wvl / wvr not allocated)
     // d-sharded WTA (more than one shard in the frame)
     int64_t *key = nullptr, *key_g = nullptr, *tkey = nullptr, *tkey_g = nullptr;
     float *m1 = nullptr, *m2 = nullptr, *t1 = nullptr, *t2 = nullptr, *m2_g = nullptr, *t2_g = nullptr;
@@ -273,12 +275,21 @@ int alloc_shard(Shard &s, bool sharded) {
     // ASW_FLAG_SUPPORT_INDEX (both directions) or ASW_FLAG_SUPPORT_INDEX_V (the V passes only)
     const bool idx_on = p->flags & (ASW_FLAG_SUPPORT_INDEX | ASW_FLAG_SUPPORT_INDEX_V);
     const bool v_only = !(p->flags & ASW_FLAG_SUPPORT_INDEX);
-    s.vidx = idx_on && asw_pass_index_supported(p, ASW_DIR_V, ASW_DEN_NONE) != 0;
+    // ASW_FLAG_OTF_V, a 32-plane shard's V passes compute both weights from
+    // the images and the LUT (asw_aggregate_pass_otf_v; the V arrays are never built)
+    s.otfv = (p->flags & ASW_FLAG_OTF_V) && asw_pass_otf_v_supported(p) != 0;
+    s.vidx = !s.otfv && idx_on && asw_pass_index_supported(p, ASW_DIR_V, ASW_DEN_NONE) != 0;
     s.hidx = idx_on && !v_only && s.vidx && asw_pass_index_supported(p, ASW_DIR_H, ASW_DEN_READ) != 0;
+    // the raw-cost volume as uint16 (half the bytes written by asw_Aggr and read by the
+    // first V pass; bit-identical), where built and not replaced by the fused or
+    // index-form first pass; ASW_FLAG_RAW_F32 keeps the float volume
+    s.raw16 = !s.fuse && !s.vidx && !s.otfv && !(p->flags & ASW_FLAG_RAW_F32) && asw_raw16_supported(p);
     const size_t vbytes = s.vidx ? asw_support_index_bytes(p) : asw_support_bytes(p);
     const size_t hbytes = s.hidx ? asw_support_index_bytes(p) : asw_support_bytes(p);
-    ASWCHK(dev_alloc(&s.wvl, vbytes));
-    ASWCHK(dev_alloc(&s.wvr, vbytes));
+    if (!s.otfv) {
+        ASWCHK(dev_alloc(&s.wvl, vbytes));
+        ASWCHK(dev_alloc(&s.wvr, vbytes));
+    }
     ASWCHK(dev_alloc(&s.whl, hbytes));
     // the right H weights can be computed inside the H passes
     // (asw_aggregate_pass_otf, the array then never built): bit-identical but measured
@@ -439,7 +450,8 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_raw], st));
     // the raw cost: its own kernel, or (s.fuse) computed inside the first V pass
-    if (!s.fuse) ASWCHK(asw_raw_cost(p, s.left, s.right, s.c0, st));
+    if (s.raw16) ASWCHK(asw_raw_cost16(p, s.left, s.right, reinterpret_cast<uint16_t *>(s.c0), st));
+    else if (!s.fuse) ASWCHK(asw_raw_cost(p, s.left, s.right, s.c0, st));
     if (timed) HIPCHK(hipEventRecord(c->ev[e_raw + 1], st));
     if (p->color_space == ASW_COLOR_LAB) {
         ASWCHK(asw_lab(p, s.left, s.lab_l, st));
@@ -450,7 +462,8 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         ASWCHK(asw_support_lab(p, ASW_DIR_H, s.lab_r, s.whr, st));
     } else {
         ASWCHK(asw_support_lut(p, s.lut, st));
-        ASWCHK(asw_support_all_fmt(p, s.left, s.right, s.lut, s.wvl, s.whl, s.wvr, s.otf ? nullptr : s.whr,
+        ASWCHK(asw_support_all_fmt(p, s.left, s.right, s.lut, s.otfv ? nullptr : s.wvl, s.whl,
+                                   s.otfv ? nullptr : s.wvr, s.otf ? nullptr : s.whr,
                                    (s.vidx ? 5 : 0) | (s.hidx ? 10 : 0), st));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0], st));
@@ -459,6 +472,11 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         const int dm = !s.den_h ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
         if (it == 0 && s.fuse)
             ASWCHK(asw_aggregate_pass_raw(p, s.wvl, s.wvr, s.left, s.right, s.c1, s.den_v, dmv, st));
+        else if (s.otfv)
+            ASWCHK(asw_aggregate_pass_otf_v(p, s.left, s.right, s.lut, s.c0, s.c1, st));
+        else if (it == 0 && s.raw16)
+            ASWCHK(asw_aggregate_pass_den16(p, s.wvl, s.wvr, reinterpret_cast<const uint16_t *>(s.c0), s.c1, s.den_v,
+                                            dmv, st));
         else if (s.vidx)
             ASWCHK(asw_aggregate_pass_index(p, ASW_DIR_V, reinterpret_cast<const uint16_t *>(s.wvl),
                                             reinterpret_cast<const uint16_t *>(s.wvr), s.lut, s.c0, s.c1, nullptr,

@@ -81,13 +81,17 @@ __global__ void k_support_lut(float *lut, int rows, float gamma_c, float gamma_g
 // pixels they reach (columns x - d) are staged once in LDS, so each lane's four
 // planes d = 4q..4q+3 read LDS instead of four gathers; the left pixel is
 // wave-uniform.  Every store is a float4 per lane (1 KB per wave-instruction).
+// U16 (asw_raw_cost16): the same costs as uint16 (an integer AD <= 765, or its
+// truncation at an integral tau), a 4 x uint16 store per lane: half the bytes.
 // ---------------------------------------------------------------------------
 constexpr int kRawPPW = 16;                       // pixels per wave
 constexpr int kRawSpan = 4 * kRawPPW;              // pixels per block
+template <bool U16>
 __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, const uchar4 *__restrict__ R,
-                                                   float *__restrict__ cost, int W, int Dp, int nloc, int d_begin,
+                                                   void *__restrict__ cost_v, int W, int Dp, int nloc, int d_begin,
                                                    float tau) {
     using f4 = float __attribute__((ext_vector_type(4)));
+    using u4 = unsigned short __attribute__((ext_vector_type(4)));
     // R[y][xr], xr in [xlo, x0 + kRawSpan), in 4 phases: element t at (t & 3) * s4 +
     // (t >> 2).  The lanes of a read are 4 elements apart (planes 4q..4q+3 of lane q),
     // so they read consecutive dwords of one phase (a linear row: 4-way conflicts), and
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
     const int lpp = ppi > 1 ? nq : 64;  // lanes per pixel
     for (int x = xa + lane / lpp; x < xb; x += ppi) {
         const uchar4 l = Lrow[x];
-        f4 *out = reinterpret_cast<f4 *>(cost + ((long long)y * W + x) * Dp);
+        const long long e0 = ((long long)y * W + x) * Dp;  // first element of pixel x
         for (int q = lane % lpp; q < nq; q += lpp) {
             f4 v;
 #pragma unroll
@@ -126,7 +130,14 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
                 sv = sv + fabsf((float)l.z - (float)r.z);
                 v[j] = k < nloc ? fminf(sv, tau) : 0.0f;
             }
-            out[q] = v;
+            if constexpr (U16) {
+                u4 h;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) h[j] = (unsigned short)v[j];  // exact: integers in [0, 765]
+                reinterpret_cast<u4 *>(static_cast<unsigned short *>(cost_v) + e0)[q] = h;
+            } else {
+                reinterpret_cast<f4 *>(static_cast<float *>(cost_v) + e0)[q] = v;
+            }
         }
     }
 }
@@ -148,25 +159,16 @@ struct SupportJobs {
     int dir[4];
     int idx[4];   // 1: write the LUT index dist*766 + SAD of each weight (asw_support_all_fmt)
 };
-// EXPD: each weight computed as k_support_lut computes the table entry, (float)
-// exp_d((double)(c_diff[SAD] - g_dist[dist])) with the two float quotients tabulated
-// per block in LDS (766 + R+1 entries), instead of gathered from the LUT: the same
-// value bit for bit, no dependent image -> LUT gather chain (~20 double-precision
-// VALU per weight instead).
-template <int Q, bool EXPD = false>
+// (Round 4's EXPD form, each weight's exp computed instead of gathered, measured
+// slower and moved to tools/exp/exp_forms.hip.)
+template <int Q>
 __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *__restrict__ lut, int W, int H,
-                                                 int T, float gamma_c = 1.0f, float gamma_g = 1.0f) {
+                                                 int T) {
     using f4 = float __attribute__((ext_vector_type(4)));
     // 4 waves x 64 pixels x Q float4 = 4 KiB per Q: Q = 17 (T 65-68) takes 68 KiB,
     // which only the 160 KiB LDS of gfx950 holds (the build targets gfx950 only)
     static_assert(4 * 64 * Q * 16 <= 160 * 1024, "k_support staging tile exceeds the gfx950 LDS");
     __shared__ f4 stg[4][64 * Q];  // per wave: its 64 pixels' Q float4, in output order
-    __shared__ float cd_s[EXPD ? kLutWidth : 1], gd_s[EXPD ? 2 * Q + 1 : 1];  // (R <= 2Q)
-    if constexpr (EXPD) {  // (before any wave leaves: the one barrier)
-        for (int t = threadIdx.x; t < kLutWidth; t += 256) cd_s[t] = (float)(-t) / gamma_c;  // K/asw_vsupport.cl:22
-        for (int t = threadIdx.x; t <= T / 2; t += 256) gd_s[t] = (float)t / gamma_g;        // :24
-        __syncthreads();
-    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x0 = blockIdx.x * 64;
     const int y = blockIdx.y * 4 + wv;
@@ -234,8 +236,7 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
                 dist = x > qx ? x - qx : qx - x;
             }
             const int sad = abs((int)a.x - (int)b[k].x) + abs((int)a.y - (int)b[k].y) + abs((int)a.z - (int)b[k].z);
-            if constexpr (EXPD) v[k / 4][k % 4] = k < T ? (float)exp_d((double)(cd_s[sad] - gd_s[dist])) : 0.0f;
-            else v[k / 4][k % 4] = k < T ? lut[dist * kLutWidth + sad] : 0.0f;
+            v[k / 4][k % 4] = k < T ? lut[dist * kLutWidth + sad] : 0.0f;
         }
         // The wave's 64 pixels are one contiguous 64*Q-float4 run of the output:
         // transposed through LDS (Q odd: the 144-B lane stride of the writes is
@@ -289,18 +290,11 @@ __global__ __launch_bounds__(256) void k_support_any(SupportJobs jobs, const flo
     reinterpret_cast<f4 *>(jobs.w[blockIdx.z] + (long long)y * W * Tp)[t] = v;
 }
 
-// asw_tune_set(ASW_TUNE_PASS_VARIANT) bit 27: k_support computes each weight's exp
-// instead of gathering it from the LUT (EXPD)
-int g_support_expd = 0;
 template <int Q>
 void launch_support_q(const asw_params *p, const SupportJobs &jobs, int njobs, const float *lut,
                              hipStream_t st) {
     const dim3 grid((unsigned)((p->width + 63) / 64), (unsigned)((p->height + 3) / 4), (unsigned)njobs);
-    if (g_support_expd)
-        hipLaunchKernelGGL((k_support<Q, true>), grid, dim3(256), 0, st, jobs, lut, p->width, p->height, p->taps,
-                           p->gamma_c, p->gamma_g);
-    else hipLaunchKernelGGL((k_support<Q, false>), grid, dim3(256), 0, st, jobs, lut, p->width, p->height, p->taps,
-                            p->gamma_c, p->gamma_g);
+    hipLaunchKernelGGL((k_support<Q>), grid, dim3(256), 0, st, jobs, lut, p->width, p->height, p->taps);
 }
 
 // ---------------------------------------------------------------------------
@@ -370,159 +364,17 @@ __global__ __launch_bounds__(256) void k_support_lab(const float4 *__restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// WTA top-2 state: first minimum m1 (index idx) and the second smallest m2 of
-// the multiset, strict '<' in scan order (K/asw_wta.cl:43-46).  Partial states
-// over disjoint index sets combine exactly and order-independently:
-// m1 = lexicographic min of (value, index); m2 = min(max(m1a,m1b), m2a, m2b).
+// WTA: first minimum m1 (index idx) and the second smallest m2 of the multiset,
+// strict '<' in scan order (K/asw_wta.cl:43-46); the scans are lane-per-pixel
+// (asw_refine.hip).  (The wave-per-pixel WTA kernels of round 1, which combined
+// partial states by shuffles, are in tools/exp/exp_forms.hip.)
 // ---------------------------------------------------------------------------
-struct Top2 {
-    float m1, m2;
-    int idx;
-};
-
-__device__ __forceinline__ void top2_update(Top2 &s, float t, int d) {
-    s.m2 = t < s.m2 ? t : s.m2;
-    s.idx = t < s.m1 ? d : s.idx;
-    s.m2 = t < s.m1 ? s.m1 : s.m2;
-    s.m1 = t < s.m1 ? t : s.m1;
-}
-
-__device__ __forceinline__ void top2_combine(Top2 &a, float om1, float om2, int oidx) {
-    const float nm2 = fminf(fmaxf(a.m1, om1), fminf(a.m2, om2));
-    const bool take = (om1 < a.m1) || (om1 == a.m1 && oidx < a.idx);
-    a.m1 = take ? om1 : a.m1;
-    a.idx = take ? oidx : a.idx;
-    a.m2 = nm2;
-}
-
-__device__ __forceinline__ void top2_wave_reduce(Top2 &s) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const float om1 = __shfl_xor(s.m1, off, 64);
-        const float om2 = __shfl_xor(s.m2, off, 64);
-        const int oidx = __shfl_xor(s.idx, off, 64);
-        top2_combine(s, om1, om2, oidx);
-    }
-}
-
 constexpr float kInit = 100000.0f;  // K/asw_wta.cl:25-26
-
-// Pixel of this wave in the WTA kernels: blocks of 4 waves = 4 consecutive
-// pixels; XCD j (blockIdx % 8) walks its own contiguous range of pixels in
-// order, so the row a target scan re-reads (the diagonal of the volume) was just
-// streamed through that XCD's L2 by the same XCD's main scans.
-__device__ __forceinline__ long long wta_pixel(int blocks_per_xcd) {
-    const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
-    return ((long long)xcd * blocks_per_xcd + m) * 4 + (threadIdx.x >> 6);
-}
-
-// asw_WTA_REF's scanned value (K/asw_wta_ref.cl:28): 0.085f * den * fabs(val - i) + cost,
-// left to right, uncontracted; i = the candidate's scan index
-__device__ __forceinline__ float ref_penalty(float a, float val, int i, float c) {
-    const float b = fabsf(val - (float)i);
-    return a * b + c;
-}
-
-// Target (right-view) scan of asw_WTA (K/asw_wta.cl:50-67): for i < md,
-// xq = max(0,x-i), b = md + xq - x (the bresenham() line of :3-9 always has
-// slope 1), candidate C[b][y][xq].  Only b in [b_lo, b_hi) (the local shard) is
-// visited; `index` is i so ties keep the smallest i like the sequential scan.
-// pen = true: asw_WTA_REF's target scan, value a*|val - i| + cost (K/asw_wta_ref.cl:39-57)
-__device__ __forceinline__ Top2 target_scan(const float *__restrict__ cost, int x, int y, int W, int Dp, int md,
-                                            int b_lo, int b_hi, int lane, bool pen = false, float a = 0.0f,
-                                            float val = 0.0f) {
-    Top2 s{kInit, kInit, INT_MAX};
-    for (int i = lane; i < md; i += 64) {
-        const int xq = x - i < 0 ? 0 : x - i;
-        const int b = md + xq - x;
-        if (b >= b_lo && b < b_hi) {
-            float t = cost[((long long)y * W + xq) * Dp + (b - b_lo)];
-            if (pen) t = ref_penalty(a, val, i, t);
-            top2_update(s, t, i);
-        }
-    }
-    top2_wave_reduce(s);
-    return s;
-}
-
-// asw_WTA (K/asw_wta.cl:12-82) for a context owning all D planes.
-// One wave per pixel: lanes scan d = lane, lane+64, ... then a shuffle reduction.
-__global__ __launch_bounds__(256) void k_wta(const float *__restrict__ cost, int W, int H, int Dp, int D, int bpx,
-                                             int32_t *__restrict__ d_ref, float *__restrict__ conf_ref,
-                                             int32_t *__restrict__ d_tar, float *__restrict__ conf_tar,
-                                             uint8_t *__restrict__ code_ref, uint8_t *__restrict__ code_tar) {
-    const int lane = threadIdx.x & 63;
-    const long long p = wta_pixel(bpx);
-    if (p >= (long long)W * H) return;
-    const int x = (int)(p % W), y = (int)(p / W);
-    const float *cp = cost + p * Dp;
-    Top2 s{kInit, kInit, INT_MAX};
-    for (int d = lane; d < D; d += 64) top2_update(s, cp[d], d);
-    top2_wave_reduce(s);
-    const int md = s.idx == INT_MAX ? 0 : s.idx;
-    const Top2 t = target_scan(cost, x, y, W, Dp, md, 0, D, lane);
-    if (lane == 0) {
-        const int mdr = t.idx == INT_MAX ? md : md + (x - t.idx < 0 ? 0 : x - t.idx) - x;
-        d_ref[p] = md;
-        conf_ref[p] = (s.m2 - s.m1) / s.m2;
-        d_tar[p] = mdr;
-        conf_tar[p] = (t.m2 - t.m1) / t.m2;
-        if (code_ref) code_ref[p] = (uint8_t)code_u8(md, D);
-        if (code_tar) code_tar[p] = (uint8_t)code_u8(mdr, D);
-    }
-}
 
 __device__ __forceinline__ long long make_key(float v, int idx) {
     return (long long)(((unsigned long long)__float_as_uint(v) << 32) | (unsigned)idx);
 }
 constexpr long long kNoKey = 0x7fffffffffffffffLL;
-
-// d-sharded left WTA, local half: planes [d_begin, d_end) of the shard.  ref != NULL:
-// the refinement loop's asw_WTA_REF (penalised values; ref = [2][S] value / den planes)
-__global__ __launch_bounds__(256) void k_wta_local(const float *__restrict__ cost, int W, int H, int Dp, int bpx,
-                                                   int d_begin, int nloc, long long *__restrict__ key,
-                                                   float *__restrict__ m1, float *__restrict__ m2,
-                                                   const float *__restrict__ ref) {
-    const int lane = threadIdx.x & 63;
-    const long long p = wta_pixel(bpx);
-    const long long S = (long long)W * H;
-    if (p >= S) return;
-    const float *cp = cost + p * Dp;
-    Top2 s{kInit, kInit, INT_MAX};
-    if (ref) {
-        const float a = 0.085f * ref[S + p], val = ref[p];
-        for (int k = lane; k < nloc; k += 64) top2_update(s, ref_penalty(a, val, d_begin + k, cp[k]), d_begin + k);
-    } else {
-        for (int k = lane; k < nloc; k += 64) top2_update(s, cp[k], d_begin + k);
-    }
-    top2_wave_reduce(s);
-    if (lane == 0) {
-        key[p] = s.idx == INT_MAX ? kNoKey : make_key(s.m1, s.idx);
-        m1[p] = s.m1;
-        m2[p] = s.m2;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_wta_target_local(const float *__restrict__ cost, int W, int H, int Dp, int bpx,
-                                                          int d_begin, int d_end,
-                                                          const long long *__restrict__ key_ref,
-                                                          long long *__restrict__ tkey, float *__restrict__ t1,
-                                                          float *__restrict__ t2, const float *__restrict__ ref) {
-    const int lane = threadIdx.x & 63;
-    const long long p = wta_pixel(bpx);
-    const long long S = (long long)W * H;
-    if (p >= S) return;
-    const int x = (int)(p % W), y = (int)(p / W);
-    const long long kr = key_ref[p];
-    const int md = kr == kNoKey ? 0 : (int)(unsigned)(kr & 0xffffffffLL);
-    const Top2 t = ref ? target_scan(cost, x, y, W, Dp, md, d_begin, d_end, lane, true, 0.085f * ref[S + p], ref[p])
-                       : target_scan(cost, x, y, W, Dp, md, d_begin, d_end, lane);
-    if (lane == 0) {
-        tkey[p] = t.idx == INT_MAX ? kNoKey : make_key(t.m1, t.idx);
-        t1[p] = t.m1;
-        t2[p] = t.m2;
-    }
-}
 
 // second-smallest contribution: the shard that owns the global minimum offers
 // its own second smallest, every other shard its minimum.
@@ -642,6 +494,10 @@ namespace asw {
 bool pass_index_supported(const asw_params *p, int dir, int dm);
 int launch_pass_index(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
                       const float *cin, float *cout, float *den, int dm, hipStream_t st);
+// asw_aggregate.hip: the shard V pass with both weights on the fly
+bool pass_otf_v_supported(const asw_params *p);
+int launch_pass_otf_v(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut,
+                      const float *cin, float *cout, hipStream_t st);
 // asw_wta_sweep.hip: asw_WTA as a row sweep (ASW_E_UNSUPPORTED for pitches it is not built for)
 int launch_wta_sweep(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
                      float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, hipStream_t st);
@@ -654,24 +510,22 @@ extern "C" {
 // 3: asw_params.flags (round 5)
 int asw_abi_version(void) { return ASW_ABI_VERSION; }
 
-// 0: lane-per-pixel scans (default), 1: wave per pixel, 2: asw_WTA by the row sweep
-// (asw_wta_sweep.hip; the sharded halves keep the lane-per-pixel scans)
+// 0: lane-per-pixel scans (default), 2: asw_WTA by the row sweep (asw_wta_sweep.hip;
+// the sharded halves keep the lane-per-pixel scans).  1 (round 1's wave per pixel) is
+// no longer built (tools/exp/exp_forms.hip)
 static int g_wta_variant = 0;
 
 int asw_tune_set(int key, int value) {
     if (key == ASW_TUNE_PASS_VARIANT) {
         // only bits that select a compiled form (launch_dm): a stale bit would time the
         // default kernel under another name
-        // (+ bits 16-26: strip / segment counts, the lean H form and its ring, and the
-        // index-form H phases of the 32-plane shard passes, asw_pass32.h)
-        // (bit 27: the support kernel's EXPD form, k_support)
-        if (value & ~(asw::kPassVariantBits | 0xFFF0000)) return ASW_E_INVALID;
-        const int old_expd = asw::g_support_expd;
-        asw::g_support_expd = (value >> 27) & 1;
-        return asw::set_pass_variant(value & ~(1 << 27)) | (old_expd << 27);
+        // (+ bits 16-26: strip / segment counts, the H form, the index-form H phases and
+        // the nt policy flip of the 32-plane shard passes, asw_pass32.h)
+        if (value & ~(asw::kPassVariantBits | 0x7FF0000)) return ASW_E_INVALID;
+        return asw::set_pass_variant(value);
     }
     if (key == ASW_TUNE_WTA_VARIANT) {
-        if (value < 0 || value > 2) return ASW_E_INVALID;
+        if (value != 0 && value != 2) return ASW_E_INVALID;
         const int old = g_wta_variant;
         g_wta_variant = value;
         return old;
@@ -752,17 +606,42 @@ size_t asw_lut_bytes(const asw_params *p) { return (size_t)(p->taps / 2 + 1) * k
         if (_s != ASW_OK) return _s;         \
     } while (0)
 
-int asw_raw_cost(const asw_params *p, const uint8_t *left, const uint8_t *right, float *cost, void *stream) {
-    ASW_CHECK_PARAMS(p);
-    if (!left || !right || !cost) return ASW_E_INVALID;
+static int launch_raw_cost(bool u16, const asw_params *p, const uint8_t *left, const uint8_t *right, void *cost,
+                           void *stream) {
     const int Dp = asw_disp_pitch(p);
     const dim3 grid((unsigned)((p->width + kRawSpan - 1) / kRawSpan), (unsigned)p->height);
     const size_t lds = (size_t)4 * (((kRawSpan + Dp - 1 + 3) / 4 + 31) / 32 * 32 + 8) * 4;  // 4 phases of s4
     if (lds > 64 * 1024) return ASW_E_UNSUPPORTED;
-    hipLaunchKernelGGL(k_raw_cost, grid, dim3(256), lds, (hipStream_t)stream, reinterpret_cast<const uchar4 *>(left),
-                       reinterpret_cast<const uchar4 *>(right), cost, p->width, Dp, d_end_of(p) - p->d_begin,
-                       p->d_begin, p->tad_tau);
+    const uchar4 *l = reinterpret_cast<const uchar4 *>(left), *r = reinterpret_cast<const uchar4 *>(right);
+    if (u16)
+        hipLaunchKernelGGL(k_raw_cost<true>, grid, dim3(256), lds, (hipStream_t)stream, l, r, cost, p->width, Dp,
+                           d_end_of(p) - p->d_begin, p->d_begin, p->tad_tau);
+    else
+        hipLaunchKernelGGL(k_raw_cost<false>, grid, dim3(256), lds, (hipStream_t)stream, l, r, cost, p->width, Dp,
+                           d_end_of(p) - p->d_begin, p->d_begin, p->tad_tau);
     return finish_launch();
+}
+
+int asw_raw_cost(const asw_params *p, const uint8_t *left, const uint8_t *right, float *cost, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!left || !right || !cost) return ASW_E_INVALID;
+    return launch_raw_cost(false, p, left, right, cost, stream);
+}
+
+// the raw costs are integers (AD <= 765) unless a non-integral tau truncates them
+static bool raw16_exact(const asw_params *p) { return p->tad_tau >= 765.0f || p->tad_tau == floorf(p->tad_tau); }
+
+int asw_raw16_supported(const asw_params *p) {
+    if (!p || asw_params_check(p) != ASW_OK) return 0;
+    // exact, and read by a ring-kernel first V pass (asw_aggregate_pass_den16)
+    return raw16_exact(p) && p->tad_tau >= 0.0f && p->iters >= 1 && asw::ring_taps(p->taps) ? 1 : 0;
+}
+
+int asw_raw_cost16(const asw_params *p, const uint8_t *left, const uint8_t *right, uint16_t *cost, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!left || !right || !cost) return ASW_E_INVALID;
+    if (!raw16_exact(p) || p->tad_tau < 0.0f) return ASW_E_UNSUPPORTED;
+    return launch_raw_cost(true, p, left, right, cost, stream);
 }
 
 int asw_support_lut(const asw_params *p, float *lut, void *stream) {
@@ -900,6 +779,18 @@ int asw_aggregate_pass_index(const asw_params *p, int dir, const uint16_t *wl, c
     return asw::launch_pass_index(p, dir, wl, wr, lut, cin, cout, den, den_mode, (hipStream_t)stream);
 }
 
+int asw_pass_otf_v_supported(const asw_params *p) {
+    if (!p || asw_params_check(p) != ASW_OK) return 0;
+    return asw::pass_otf_v_supported(p) ? 1 : 0;
+}
+
+int asw_aggregate_pass_otf_v(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba,
+                             const float *lut, const float *cin, float *cout, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!left_rgba || !right_rgba || !lut || !cin || !cout || cin == cout) return ASW_E_INVALID;
+    return asw::launch_pass_otf_v(p, left_rgba, right_rgba, lut, cin, cout, (hipStream_t)stream);
+}
+
 int asw_pass_index_supported(const asw_params *p, int dir, int den_mode) {
     if (!p || asw_params_check(p) != ASW_OK) return 0;
     return asw::pass_index_supported(p, dir, den_mode) ? 1 : 0;
@@ -916,6 +807,17 @@ int asw_pass_raw_supported(const asw_params *p) {
     if (!p || asw_params_check(p) != ASW_OK) return 0;
     // ring kernels only (in a make DEV=1 library: its one tap count), not a 32-plane shard
     return p->iters >= 1 && asw::ring_taps(p->taps) && asw_disp_pitch(p) != 32 ? 1 : 0;
+}
+
+int asw_aggregate_pass_den16(const asw_params *p, const float *wvl, const float *wvr, const uint16_t *cin16,
+                             float *cout, float *den, int den_mode, void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!wvl || !wvr || !cin16 || !cout || (const void *)cin16 == (const void *)cout) return ASW_E_INVALID;
+    if (den_mode != ASW_DEN_NONE && den_mode != ASW_DEN_WRITE) return ASW_E_INVALID;  // a first pass
+    if (den_mode != ASW_DEN_NONE && (!den || den == cout)) return ASW_E_INVALID;
+    if (!asw_raw16_supported(p)) return ASW_E_UNSUPPORTED;
+    const asw::RawSrc raw{nullptr, nullptr, cin16};
+    return asw::launch_pass(p, ASW_DIR_V, wvl, wvr, nullptr, cout, den, den_mode, (hipStream_t)stream, &raw);
 }
 
 int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
@@ -958,75 +860,39 @@ int asw_wta(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_
                                             (hipStream_t)stream);
         if (s != ASW_E_UNSUPPORTED) return s;
     }
-    if (g_wta_variant != 1)
-        return asw::launch_wta_scan(p, 0, cost, nullptr, nullptr, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar,
+    return asw::launch_wta_scan(p, 0, cost, nullptr, nullptr, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar,
                                     (hipStream_t)stream);
-    const long long n = (long long)p->width * p->height;
-    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
-    hipLaunchKernelGGL(k_wta, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost, p->width,
-                       p->height, asw_disp_pitch(p), p->ndisp, bpx, d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar);
-    return finish_launch();
 }
 
 int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m1, float *m2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !key || !m1 || !m2) return ASW_E_INVALID;
-    if (g_wta_variant != 1)
-        return asw::launch_wta_local_scan(p, cost, nullptr, reinterpret_cast<long long *>(key), m1, m2,
+    return asw::launch_wta_local_scan(p, cost, nullptr, reinterpret_cast<long long *>(key), m1, m2,
                                           (hipStream_t)stream);
-    const long long n = (long long)p->width * p->height;
-    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
-    hipLaunchKernelGGL(k_wta_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
-                       p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p) - p->d_begin,
-                       reinterpret_cast<long long *>(key), m1, m2, nullptr);
-    return finish_launch();
 }
 
 int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *key_ref, int64_t *tkey, float *t1,
                          float *t2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
-    if (g_wta_variant != 1)
-        return asw::launch_wta_target_local_scan(p, cost, reinterpret_cast<const long long *>(key_ref), nullptr,
+    return asw::launch_wta_target_local_scan(p, cost, reinterpret_cast<const long long *>(key_ref), nullptr,
                                                  reinterpret_cast<long long *>(tkey), t1, t2, (hipStream_t)stream);
-    const long long n = (long long)p->width * p->height;
-    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
-    hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
-                       p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p),
-                       reinterpret_cast<const long long *>(key_ref), reinterpret_cast<long long *>(tkey), t1, t2,
-                       nullptr);
-    return finish_launch();
 }
 
 int asw_wta_ref_local(const asw_params *p, const float *cost, const float *ref_l, int64_t *key, float *m1, float *m2,
                       void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !ref_l || !key || !m1 || !m2) return ASW_E_INVALID;
-    if (g_wta_variant != 1)
-        return asw::launch_wta_local_scan(p, cost, ref_l, reinterpret_cast<long long *>(key), m1, m2,
+    return asw::launch_wta_local_scan(p, cost, ref_l, reinterpret_cast<long long *>(key), m1, m2,
                                           (hipStream_t)stream);
-    const long long n = (long long)p->width * p->height;
-    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
-    hipLaunchKernelGGL(k_wta_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
-                       p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p) - p->d_begin,
-                       reinterpret_cast<long long *>(key), m1, m2, ref_l);
-    return finish_launch();
 }
 
 int asw_wta_ref_target_local(const asw_params *p, const float *cost, const float *ref_r, const int64_t *key_ref,
                              int64_t *tkey, float *t1, float *t2, void *stream) {
     ASW_CHECK_PARAMS(p);
     if (!cost || !ref_r || !key_ref || !tkey || !t1 || !t2) return ASW_E_INVALID;
-    if (g_wta_variant != 1)
-        return asw::launch_wta_target_local_scan(p, cost, reinterpret_cast<const long long *>(key_ref), ref_r,
+    return asw::launch_wta_target_local_scan(p, cost, reinterpret_cast<const long long *>(key_ref), ref_r,
                                                  reinterpret_cast<long long *>(tkey), t1, t2, (hipStream_t)stream);
-    const long long n = (long long)p->width * p->height;
-    const int bpx = (int)(((n + 3) / 4 + 7) / 8);
-    hipLaunchKernelGGL(k_wta_target_local, dim3((unsigned)(8 * bpx)), dim3(256), 0, (hipStream_t)stream, cost,
-                       p->width, p->height, asw_disp_pitch(p), bpx, p->d_begin, d_end_of(p),
-                       reinterpret_cast<const long long *>(key_ref), reinterpret_cast<long long *>(tkey), t1, t2,
-                       ref_r);
-    return finish_launch();
 }
 
 int asw_wta_ref_finalize(const asw_params *p, const int64_t *key, const int64_t *tkey, const float *t2,

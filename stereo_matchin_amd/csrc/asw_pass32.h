@@ -53,7 +53,19 @@ __device__ __forceinline__ void taps32(float &num, float &den, const f4 (&wl)[M]
 // half the bytes): the block copies the LUT into LDS once and each staged float4 is
 // looked up there (4 ds_read_b32) before it enters the slab ring; the taps then run
 // on the same float weights, so the result is bit-identical.
-template <int T, int NW, int DM, int CP, int NPH, bool IDX = false, int RB = 2, int PS = 4>
+// C16: the first V pass over the uint16 raw costs (asw_raw_cost16), as k_vpass10<C16>.
+// OTF: both support weights of a slab row computed in the pass from the
+// two images and the LUT (wl / wr are the left / right RGBA8 images, lut the global
+// asw_support_lut table), so the V support arrays are never built nor read.  The
+// staging shares are assigned tap-group-major (a wave's lanes = consecutive entries of
+// one float4 group q): each pixel load is one row's consecutive pixels and the LUT
+// gathers of a wave fall in one 3-KB LUT row (dist = |4q + j - R| but at the image
+// edges).  Each weight is k_support's: lut[|y - qy|][SAD(img(y, c), img(qy, c))],
+// qy = clamp(y + i - R), 0 for taps i >= T, so the slab holds the same floats.
+// Pipeline: the pixels of a row are loaded PSO steps before its gathers, which are
+// issued one step before the row is written to the slab.
+template <int T, int NW, int DM, int CP, int NPH, bool IDX = false, int RB = 2, int PS = 4, bool C16 = false,
+          bool OTF = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 4 : 2))) void k_vpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
     float *__restrict__ den, int W, int H, int d_begin, int rows_per_strip, int nxb, int nstrip, int xg_per_xcd,
@@ -67,7 +79,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     constexpr int LEAD = RB + 1;
     constexpr int NBUF = ring_div(U, 2 * RB + 1);
     static_assert(U % PS == 0 && U % KD == 0 && U % RB == 0 && U % NBUF == 0, "ring periods");
-    static_assert(LEAD <= PS, "staging ring too short for the barrier period");
+    static_assert(OTF || LEAD <= PS, "staging ring too short for the barrier period");
+    static_assert(!OTF || (!IDX && !C16 && TP == 4 * Q), "on-the-fly weights: float supports, float input");
+    constexpr int PSO = 2;  // OTF: rows of pixels in flight
+    static_assert(!OTF || U % PSO == 0, "pixel ring period");
     constexpr int LA = cmax(cmax(R + P, LEAD + PS), KD);  // rows past y a step touches
     constexpr int NC = 2 * NW;                             // columns per block
     constexpr int NER = NC + 31;                           // right entries per row
@@ -101,6 +116,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     auto rsrc_at = [&](const float *base, int row) __attribute__((always_inline)) {
         return make_rsrc(base + (long long)row * rowstride + colbase);
     };
+    auto cin_at = [&](int row) __attribute__((always_inline)) {
+        if constexpr (C16) return make_rsrc(reinterpret_cast<const uint16_t *>(cin) + (long long)row * rowstride + colbase);
+        else return rsrc_at(cin, row);
+    };
+    auto cload = [&](rsrc_t r, int off) __attribute__((always_inline)) {  // off: bytes of the float volume
+        if constexpr (C16) return bload16<CP>(r, voff >> 1, off >> 1);
+        else return bload<CP>(r, voff, off);
+    };
+    // C16: window elements in flight stay integers (a P-deep ring), converted the step
+    // they enter the window, as k_vpass10<C16>
+    auto cload_raw = [&](rsrc_t r, int off) __attribute__((always_inline)) {
+        return (unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, voff >> 1, off >> 1, CP);
+    };
+    constexpr int PR = ring_div(U, P);  // (a divisor of U: compile-time slots in every chunk)
+    unsigned r16[C16 ? PR : 1];         // the load of step s sits in slot s mod PR until step s + P
 
     // slab row staging: thread share t0 (t1) = float4 q of entry e; entries < NER are
     // right weights of xr = x0 - d_begin - 31 + e, the rest left weights of column
@@ -116,6 +146,36 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     };
     const int o0 = src_of(t0), o1 = src_of(t1);
     const bool r0 = t0 / Q < NER, r1 = t1 / Q < NER;
+    // OTF: thread t computes share (q = t / NE, entry e = t % NE), stored at slab index
+    // e * Q + q (the layout above); its pixel column and image, and its taps 4q .. 4q+3
+    const int ot = min((int)threadIdx.x, NQ - 1);
+    const int oq = ot / NE, oe = ot - oq * NE;
+    const int oslot = oe * Q + oq;
+    const int ocol = oe < NER ? clampi(x0 - d_begin - 31 + oe, 0, W - 1) : min(x0 + oe - NER, W - 1);
+    const unsigned *__restrict__ oimg = reinterpret_cast<const unsigned *>(oe < NER ? wr : wl);
+    struct Px {
+        unsigned c, n[4];  // RGBA8 of the entry pixel at row y and of its taps' rows
+    };
+    auto px_load = [&](int row) __attribute__((always_inline)) {
+        Px v;
+        v.c = oimg[(long long)row * W + ocol];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v.n[j] = oimg[(long long)clampi(row + 4 * oq + j - R, 0, H - 1) * W + ocol];
+        return v;
+    };
+    auto px_gather = [&](const Px &v, int row) __attribute__((always_inline)) {
+        f4 w;
+        const unsigned c = v.c & 0xFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 4 * oq + j;
+            const int qy = clampi(row + i - R, 0, H - 1);
+            const int dist = row > qy ? row - qy : qy - row;
+            const unsigned sad = __builtin_amdgcn_sad_u8(c, v.n[j] & 0xFFFFFFu, 0u);  // |dR|+|dG|+|dB|
+            w[j] = i < T ? lut[dist * kLutWidth + (int)sad] : 0.0f;
+        }
+        return w;
+    };
     // staged share: 4 weights (f4) or 4 LUT indices (u2, two uint16 per dword)
     using stg_t = std::conditional_t<IDX, u2, f4>;
     using elem_t = std::conditional_t<IDX, uint16_t, float>;
@@ -149,26 +209,51 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
 
     using PH = Phases<T, NPH>;
     float win[U];
-    stg_t sa[PS], sb[PS];
+    stg_t sa[OTF ? 1 : PS], sb[OTF ? 1 : PS];
+    Px px[OTF ? PSO : 1];
+    f4 gw;  // OTF: the gathered weights of the row written to the slab at the next step
     f4 wlp[NPH][PH::NG], wrp[NPH][PH::NG];
     float dring[KD];
     {
         const int r0 = max(0, y_begin - R);
-        const rsrc_t rp = rsrc_at(cin, r0);
+        const rsrc_t rp = cin_at(r0);
 #pragma unroll
-        for (int j = 0; j < U - 1; ++j) win[j] = bload<CP>(rp, voff, (clampi(y_begin - R + j, 0, H - 1) - r0) * rowbytes);
+        for (int j = 0; j < U - 1; ++j) {
+            const int off = (clampi(y_begin - R + j, 0, H - 1) - r0) * rowbytes;
+            if constexpr (C16) {
+                if (j < T - 1) win[j] = cload(rp, off);
+                else r16[(j - (T - 1) - P + PR) % PR] = cload_raw(rp, off);  // "loaded" at step j-(T-1)-P
+            } else {
+                win[j] = cload(rp, off);
+            }
+        }
     }
     if constexpr (DM == DM_READ) {
         const rsrc_t rp = rsrc_at(den, y_begin);
 #pragma unroll
         for (int j = 0; j < KD; ++j) dring[j] = bload<CP>(rp, voff, (min(y_begin + j, H - 1) - y_begin) * rowbytes);
     }
+    if constexpr (OTF) {
+        // rows 0 .. LEAD-1 into the slab, row LEAD's gathers, rows LEAD+1 .. LEAD+PSO-1's pixels
 #pragma unroll
-    for (int j = 0; j < PS; ++j) stage(sa[j], sb[j], min(y_begin + j, H - 1));
+        for (int j = 0; j < LEAD; ++j) {
+            const int row = min(y_begin + j, H - 1);
+            slab[j][oslot] = px_gather(px_load(row), row);
+        }
+        {
+            const int row = min(y_begin + LEAD, H - 1);
+            gw = px_gather(px_load(row), row);
+        }
 #pragma unroll
-    for (int j = 0; j < LEAD; ++j) put(j, weights(sa[j]), weights(sb[j]));
+        for (int j = LEAD + 1; j < LEAD + PSO; ++j) px[j % PSO] = px_load(min(y_begin + j, H - 1));
+    } else {
 #pragma unroll
-    for (int j = 0; j < LEAD; ++j) stage(sa[j], sb[j], min(y_begin + PS + j, H - 1));
+        for (int j = 0; j < PS; ++j) stage(sa[j], sb[j], min(y_begin + j, H - 1));
+#pragma unroll
+        for (int j = 0; j < LEAD; ++j) put(j, weights(sa[j]), weights(sb[j]));
+#pragma unroll
+        for (int j = 0; j < LEAD; ++j) stage(sa[j], sb[j], min(y_begin + PS + j, H - 1));
+    }
     __syncthreads();
     auto request = [&](auto kc, int buf) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
@@ -183,7 +268,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
         constexpr bool CLAMP = decltype(mode_c)::value >= 1;
         constexpr bool PART = decltype(mode_c)::value == 2;
         const int cb = min(ys + R + P, H - 1);
-        const rsrc_t rc = rsrc_at(cin, cb);
+        const rsrc_t rc = cin_at(cb);
         const rsrc_t ro = rsrc_at(cout, ys);
         const rsrc_t rd = rsrc_at(den, ys);
         const rsrc_t rdn = rsrc_at(den, min(ys + KD, H - 1));
@@ -196,6 +281,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
             }
             constexpr int bcur = s % NBUF, bnext = (s + 1) % NBUF, bput = (s + LEAD) % NBUF;
             float num = 1e-5f, dn = 1e-5f;
+            if constexpr (C16) win[(s + T - 1) % U] = (float)r16[(s - P + PR) % PR];  // row y+R, loaded P steps ago
             static_for<0, NPH>([&](auto kc) __attribute__((always_inline)) {
                 constexpr int k = decltype(kc)::value;
                 // (lgkmcnt 0) phase k's weights are in; at k = 0 every RB rows, also the
@@ -207,13 +293,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
                 // (IDX: the staged row's LUT reads go out before the weight requests, so
                 // the slab write waits for them alone)
                 f4 pa, pb;
-                if constexpr (k == 0) {
+                if constexpr (k == 0 && !OTF) {
                     pa = weights(sa[(s + LEAD) % PS]);
                     if constexpr (NSTAGE > 1) pb = weights(sb[(s + LEAD) % PS]);
                 }
                 if constexpr (k + 1 < NPH) request(std::integral_constant<int, k + 1>{}, bcur);
                 else request(std::integral_constant<int, 0>{}, bnext);
-                if constexpr (k == 0) {
+                if constexpr (k == 0 && OTF) {
+                    // row y+LEAD (gathered a step ago) into the slab; row y+LEAD+1's gathers;
+                    // row y+LEAD+PSO's pixels into the slot row y+LEAD's pixels held
+                    slab[bput][oslot] = gw;
+                    const int rg = min(y + LEAD + 1, H - 1);
+                    gw = px_gather(px[(s + LEAD + 1) % PSO], rg);
+                    px[(s + LEAD) % PSO] = px_load(min(y + LEAD + PSO, H - 1));
+                } else if constexpr (k == 0) {
                     put(bput, pa, pb);
                     stage(sa[(s + LEAD) % PS], sb[(s + LEAD) % PS], min(y + LEAD + PS, H - 1));
                 }
@@ -228,7 +321,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
                 bstore<CP>(dn, rd, voff, so);
             }
             bstore<CP>(div_pos(num, dn), ro, voff, so);
-            win[(s + U - 1) % U] = bload<CP>(rc, voff, CLAMP ? (min(y + R + P, H - 1) - cb) * rowbytes : so);
+            if constexpr (C16) r16[s % PR] = cload_raw(rc, CLAMP ? (min(y + R + P, H - 1) - cb) * rowbytes : so);
+            else win[(s + U - 1) % U] = cload(rc, CLAMP ? (min(y + R + P, H - 1) - cb) * rowbytes : so);
             so += rowbytes;
             asm volatile("" : "+s"(so));
         });
@@ -262,6 +356,9 @@ constexpr int h32_batch(int T) { return tap_pitch(T) / 4 * 8 <= 64 * 4 ? 4 : 2; 
 // IDX: index-form supports (uint16 LUT indices): the block's waves share one LDS copy
 // of the LUT, and each staged float4 is looked up there before it enters the ring.
 // KB: the refill batch (0: h32_batch).
+// (Round 5: the weights requested two phases ahead instead of one measured 0.3115
+// against 0.3173 ms per pass and the same shard frame, profiles/r05/pd2_nt_r12c.log;
+// not kept.)
 template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0>
 __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_hpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
@@ -477,7 +574,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 // ---------------------------------------------------------------------------
 // launchers (one (T, DM) per translation unit: build/p32_t<T>_d<DM>.hip)
 // ---------------------------------------------------------------------------
-template <int T, int NW, int DM, int CP, int NPH, bool IDX = false>
+template <int T, int NW, int DM, int CP, int NPH, bool IDX = false, bool C16 = false, bool OTF = false>
 void launch_v32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
                 hipStream_t st, const float *lut = nullptr) {
     constexpr int U = pf9_period(T);
@@ -496,9 +593,9 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
     const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
     nstrip = (H + rows - 1) / rows;
     const int per_xcd = (nxb + 7) / 8;
-    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, IDX>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl, wr,
-                       cin, cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd, lut);
-    note_pass_kernel(ASW_DIR_V, DM, "k_vpass32", T,
+    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, IDX, 2, 4, C16, OTF>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0,
+                       st, wl, wr, cin, cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd, lut);
+    note_pass_kernel(ASW_DIR_V, DM, OTF ? "k_vpass32_otf" : C16 ? "k_vpass32_c16" : "k_vpass32", T,
                      NW == 16 ? (NPH == 4 ? (IDX ? "NW=16,NPH=4,IDX" : "NW=16,NPH=4") : (IDX ? "NW=16,IDX" : "NW=16"))
                               : "NW=8,NPH=3",
                      CP == kCPStream);
@@ -533,7 +630,10 @@ template <int T, int DM>
 int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                      float *den, hipStream_t st) {
     constexpr int U = pf9_period(T);
-    const bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
+    // the nt cache policy for the cost / den / output streams from 256 MiB of volume (the
+    // C4 8-way shard, 1920 x 1080 x 32 x 4 B = 253 MiB, stays below); variant bit 26 flips it
+    bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
+    if (g_pass_variant & (1 << 26)) stream = !stream;
     if (dir == ASW_DIR_V) {
         // 16 waves (1024 threads, 4 waves per SIMD: <= 128 VGPRs): the per-lane left
         // weights take as many registers as the right ones, so T >= 33 keeps two of
@@ -565,15 +665,10 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
             if (lean) {
                 // (one-wave blocks with the conflict-free 48-entry ring, 16.7 KB of LDS, 9 per
                 // CU: C4 8-way shard frame 4.73 against 4.81-4.98 ms with the minimal 40-entry
-                // ring, 14.4 KB, 11 per CU, profiles/r04/shard_variants_r11g.log; variant bit
-                // 26 selects the minimal ring)
-                if (!(g_pass_variant & (1 << 26))) {
-                    if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
-                    else launch_h32<T, 1, DM, 0, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
-                } else {
-                    if (stream) launch_h32<T, 1, DM, kCPStream, 4, false, 3>(p, wl, wr, cin, cout, den, st, seg);
-                    else launch_h32<T, 1, DM, 0, 4, false, 3>(p, wl, wr, cin, cout, den, st, seg);
-                }
+                // ring, 14.4 KB, 11 per CU, profiles/r04/shard_variants_r11g.log; the minimal
+                // ring's lean form is no longer built, round 5)
+                if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
+                else launch_h32<T, 1, DM, 0, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
                 return finish32();
             }
         }
@@ -581,6 +676,43 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         else launch_h32<T, NWB, DM, 0, 2>(p, wl, wr, cin, cout, den, st, seg);
     }
     return finish32();
+}
+
+// the first V pass over the uint16 raw costs (asw_aggregate_pass_den16): den modes NONE
+// (what a 32-plane shard's passes run) and WRITE
+template <int T, int DM>
+int launch_pass32_c16_tm(const asw_params *p, const float *wl, const float *wr, const uint16_t *cin16, float *cout,
+                         float *den, hipStream_t st) {
+    if constexpr (DM == DM_READ) {
+        return ASW_E_INVALID;  // (never a first pass)
+    } else {
+        constexpr int NW = T > 35 ? 8 : 16;
+        constexpr int NPH = T > 35 ? 3 : T >= 33 ? 4 : 2;
+        bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
+        if (g_pass_variant & (1 << 26)) stream = !stream;
+        const float *c = reinterpret_cast<const float *>(cin16);
+        if (stream) launch_v32<T, NW, DM, kCPStream, NPH, false, true>(p, wl, wr, c, cout, den, st);
+        else launch_v32<T, NW, DM, 0, NPH, false, true>(p, wl, wr, c, cout, den, st);
+        return finish32();
+    }
+}
+
+// the V pass with both weights on the fly (asw_aggregate_pass_otf_v): T <= 35 (16-wave
+// blocks), den mode NONE (what a 32-plane shard's V passes run)
+template <int T>
+int launch_pass32_otf_v_t(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut,
+                          const float *cin, float *cout, hipStream_t st) {
+    if constexpr (T > 35) {
+        return ASW_E_UNSUPPORTED;
+    } else {
+        constexpr int NPH = T >= 33 ? 4 : 2;
+        bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
+        if (g_pass_variant & (1 << 26)) stream = !stream;
+        const float *l = reinterpret_cast<const float *>(left), *r = reinterpret_cast<const float *>(right);
+        if (stream) launch_v32<T, 16, DM_NONE, kCPStream, NPH, false, false, true>(p, l, r, cin, cout, nullptr, st, lut);
+        else launch_v32<T, 16, DM_NONE, 0, NPH, false, false, true>(p, l, r, cin, cout, nullptr, st, lut);
+        return finish32();
+    }
 }
 
 // the V pass over index-form supports (asw_aggregate_pass_index): 16-wave blocks
@@ -638,10 +770,17 @@ int launch_pass32_idx_tm(const asw_params *p, int dir, const uint16_t *wl, const
 }  // namespace agg
 }  // namespace asw
 
+#define ASW_INSTANTIATE_PASS32_OTF_V(TT)                                                                          \
+    template int asw::agg::launch_pass32_otf_v_t<TT>(const asw_params *, const uint8_t *, const uint8_t *,        \
+                                                     const float *, const float *, float *, hipStream_t);
+
 #define ASW_INSTANTIATE_PASS32_IDX(TT)                                                                            \
     template int asw::agg::launch_pass32_idx_tm<TT>(const asw_params *, int, const uint16_t *, const uint16_t *, \
-                                                    const float *, const float *, float *, float *, int, hipStream_t);
+                                                    const float *, const float *, float *, float *, int, hipStream_t); \
+    ASW_INSTANTIATE_PASS32_OTF_V(TT)
 
 #define ASW_INSTANTIATE_PASS32(TT, DM)                                                                            \
     template int asw::agg::launch_pass32_tm<TT, DM>(const asw_params *, int, const float *, const float *,       \
-                                                    const float *, float *, float *, hipStream_t);
+                                                    const float *, float *, float *, hipStream_t);               \
+    template int asw::agg::launch_pass32_c16_tm<TT, DM>(const asw_params *, const float *, const float *,        \
+                                                        const uint16_t *, float *, float *, hipStream_t);

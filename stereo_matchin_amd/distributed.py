@@ -157,7 +157,10 @@ class PipelinedMatcher:
 
     ``submit(left, right)`` returns the frame's ``MatchResult`` (valid once ``flush()``
     or a later ``submit`` into the same set has ordered the caller's stream after it:
-    ``flush()`` makes the current stream wait for every submitted tail)."""
+    ``flush()`` makes the current stream wait for every submitted tail).  Its maps and
+    images are the frame's own tensors, but ``.cost`` is the set's persistent volume:
+    the ``depth``-th later ``submit`` (the next one into the same set) overwrites it, so
+    a caller that needs the volume (e.g. for ``refine``) copies it before then."""
 
     def __init__(self, params: AswParams, rank: int = 0, world: int = 1, device="cuda", group=None, depth: int = 2):
         self.device = torch.device(device)

@@ -84,6 +84,72 @@ def asw_Aggr(p: AswParams, left: torch.Tensor, right: torch.Tensor, out: torch.T
     return out
 
 
+def otf_v_supported(p: AswParams) -> bool:
+    """asw_pass_otf_v_supported: a 32-plane shard's V pass can compute both weights on the fly."""
+    return bool(_lib.lib().asw_pass_otf_v_supported(ctypes.byref(p)))
+
+
+def asw_vCostAggregation_otf_v(p: AswParams, left: torch.Tensor, right: torch.Tensor, lut: torch.Tensor, cost_in,
+                               out=None):
+    """The V pass of a 32-plane shard with both support weights computed on the fly from
+    the images and the LUT (asw_aggregate_pass_otf_v), den mode NONE:
+    bit-identical to asw_vCostAggregation(p, asw_vSupport(p, left), asw_vSupport(p, right), ...)."""
+    _expect(left, (p.height, p.width, 4), torch.uint8, "left")
+    _expect(right, (p.height, p.width, 4), torch.uint8, "right")
+    _expect(lut, lut_shape(p), torch.float32, "lut")
+    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
+    if out is None:
+        out = new_cost(p, cost_in.device)
+    _expect(out, cost_shape(p), torch.float32, "out")
+    _lib.check(_lib.lib().asw_aggregate_pass_otf_v(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(lut), _ptr(cost_in),
+                                                   _ptr(out), _stream(cost_in.device)), "asw_aggregate_pass_otf_v")
+    return out
+
+
+def raw16_supported(p: AswParams) -> bool:
+    """asw_raw16_supported: the uint16 raw-cost volume (asw_raw_cost16) and the first V
+    pass over it (asw_aggregate_pass_den16) are built for p."""
+    return bool(_lib.lib().asw_raw16_supported(ctypes.byref(p)))
+
+
+def cost16_view(cost: torch.Tensor) -> torch.Tensor:
+    """The first half of a float cost volume's bytes as the [H][W][Dp] uint16 raw-cost
+    volume (int16 storage) that asw_Aggr16 writes and the first V pass reads."""
+    H, W, Dp = cost.shape
+    return cost.view(-1).view(torch.int16)[:H * W * Dp].view(H, W, Dp)
+
+
+def asw_Aggr16(p: AswParams, left: torch.Tensor, right: torch.Tensor, out: torch.Tensor | None = None):
+    """The raw costs of asw_Aggr (K/asw_aggr.cl:3-23) as uint16 (asw_raw_cost16: integers
+    <= 765), in int16 storage [H][W][Dp]: half the bytes of the float volume."""
+    _expect(left, (p.height, p.width, 4), torch.uint8, "left")
+    _expect(right, (p.height, p.width, 4), torch.uint8, "right")
+    if out is None:
+        out = torch.empty(cost_shape(p), dtype=torch.int16, device=left.device)
+    _expect(out, cost_shape(p), torch.int16, "out")
+    _lib.check(_lib.lib().asw_raw_cost16(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(out), _stream(left.device)),
+               "asw_raw_cost16")
+    return out
+
+
+def asw_vCostAggregation16(p: AswParams, supp_left, supp_right, cost16, out=None, den=None, den_mode: int = 0):
+    """The first vertical pass (K/asw_vcost_aggregation.cl:11-44) over the uint16 raw
+    costs of asw_Aggr16 (asw_aggregate_pass_den16; den_mode NONE or WRITE): the same
+    result as asw_vCostAggregation over asw_Aggr's float volume."""
+    _expect(supp_left, support_shape(p), torch.float32, "supp_left")
+    _expect(supp_right, support_shape(p), torch.float32, "supp_right")
+    _expect(cost16, cost_shape(p), torch.int16, "cost16")
+    if out is None:
+        out = new_cost(p, cost16.device)
+    _expect(out, cost_shape(p), torch.float32, "out")
+    if den is not None:
+        _expect(den, cost_shape(p), torch.float32, "den")
+    _lib.check(_lib.lib().asw_aggregate_pass_den16(ctypes.byref(p), _ptr(supp_left), _ptr(supp_right), _ptr(cost16),
+                                                   _ptr(out), _ptr(den), den_mode, _stream(cost16.device)),
+               "asw_aggregate_pass_den16")
+    return out
+
+
 def support_lut(p: AswParams, device, out: torch.Tensor | None = None) -> torch.Tensor:
     """(R+1) x 766 table of exp(-sad/gamma_c - dist/gamma_g) (K/asw_vsupport.cl:22-25)."""
     if out is None:

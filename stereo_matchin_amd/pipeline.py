@@ -49,7 +49,7 @@ class StereoMatcher:
     other r-1 (ASW_DEN_*); bit-identical results, 2 more cost-sized buffers."""
 
     def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool | None = None,
-                 otf: bool | None = None, support_index: bool | str | None = None):
+                 otf: bool | None = None, support_index: bool | str | None = None, otf_v: bool | None = None):
         st = _lib.params_check(params)
         if st != _lib.ASW_OK:
             raise _lib.AswError(st, "asw_params_check")
@@ -73,8 +73,16 @@ class StereoMatcher:
         self.otf = bool(otf) and K.otf_supported(self.p)
         # otf: a matcher-owned copy of the right image (the H passes read it after
         # raw_and_support returns; the caller's buffer may be reused by then)
+        # otf_v (a 32-plane shard): the V passes compute both weights from
+        # the images and the LUT (asw_aggregate_pass_otf_v), so wvl / wvr are never built.
+        # Default (None): params.flags & ASW_FLAG_OTF_V, as asw_create reads it
+        if otf_v is None:
+            otf_v = bool(params.flags & _lib.FLAG_OTF_V)
+        self.otfv = bool(otf_v) and K.otf_v_supported(self.p)
         self.right = torch.empty((self.p.height, self.p.width, 4), dtype=torch.uint8, device=dev) \
-            if self.otf else None
+            if self.otf or self.otfv else None
+        self.left = torch.empty((self.p.height, self.p.width, 4), dtype=torch.uint8, device=dev) \
+            if self.otfv else None
         # support_index (opt-in, where built: a 32-plane shard's passes): the supports in
         # index form, uint16 LUT indices (asw_support_all_fmt), half the bytes of the
         # replicated support stream; asw_aggregate_pass_index reads them.  "v": the V
@@ -85,16 +93,22 @@ class StereoMatcher:
         if want is None:  # the context flags (ASW_FLAG_SUPPORT_INDEX / _V), as asw_create reads them
             want = True if params.flags & _lib.FLAG_SUPPORT_INDEX else \
                 "v" if params.flags & _lib.FLAG_SUPPORT_INDEX_V else False
-        self.vidx = bool(want) and K.index_supported(self.p, DIR_V, _lib.DEN_NONE)
+        self.vidx = bool(want) and not self.otfv and K.index_supported(self.p, DIR_V, _lib.DEN_NONE)
         self.hidx = self.vidx and want != "v" and not self.otf and K.index_supported(self.p, DIR_H, _lib.DEN_READ)
         new_v = K.new_support_index if self.vidx else K.new_support
         new_h = K.new_support_index if self.hidx else K.new_support
-        self.wvl = new_v(self.p, dev)
-        self.wvr = new_v(self.p, dev)
+        self.wvl = None if self.otfv else new_v(self.p, dev)
+        self.wvr = None if self.otfv else new_v(self.p, dev)
         self.whl = new_h(self.p, dev)
         self.whr = None if self.otf else new_h(self.p, dev)
         self.c0 = K.new_cost(self.p, dev)
         self.c1 = K.new_cost(self.p, dev)
+        # the raw costs as uint16 in c0's first half (asw_raw_cost16 + the first V pass
+        # asw_aggregate_pass_den16: half the bytes of asw_Aggr's write and that pass's read,
+        # bit-identical), unless fused or index-form (ASW_FLAG_RAW_F32 keeps the float volume)
+        self.raw16 = (not self.fuse_raw and not self.vidx and not self.otfv and not params.flags & _lib.FLAG_RAW_F32
+                      and K.raw16_supported(self.p))
+        self.c0_16 = K.cost16_view(self.c0) if self.raw16 else None
         self.den_v = self.den_h = None
         if den_cache and self.p.iters >= 2:
             # a 32-plane shard's passes recompute den (C4 / 8: k_vpass32 den-none 0.24
@@ -112,7 +126,9 @@ class StereoMatcher:
         """asw_Aggr into c0 (unless ``raw`` is False: the first V pass computes it,
         see ``aggregate(images=...)``) and the four support arrays."""
         p = self.p
-        if raw:
+        if raw and self.raw16:
+            K.asw_Aggr16(p, left, right, out=self.c0_16)
+        elif raw:
             K.asw_Aggr(p, left, right, out=self.c0)
         if p.color_space == COLOR_LAB:
             lab_l, lab_r = K.lab_image(p, left), K.lab_image(p, right)
@@ -125,8 +141,10 @@ class StereoMatcher:
         # asw_vSupport / asw_hSupport of both images (main.cpp:469-484) in one launch
         # (without asw_hSupport(right) when the H passes compute it on the fly)
         K.support_all(p, left, right, self.lut, self.wvl, self.whl, self.wvr, self.whr)
-        if self.otf:
+        if self.otf or self.otfv:
             self.right.copy_(right.reshape(self.right.shape))
+        if self.otfv:
+            self.left.copy_(left.reshape(self.left.shape))
 
     def aggregate(self, events: list | None = None, images: tuple | None = None):
         """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515).
@@ -139,6 +157,10 @@ class StereoMatcher:
             if it == 0 and images is not None:
                 K.asw_vCostAggregation_raw(p, self.wvl, self.wvr, images[0], images[1], out=self.c1, den=self.den_v,
                                            den_mode=dmv)
+            elif self.otfv:
+                K.asw_vCostAggregation_otf_v(p, self.left, self.right, self.lut, self.c0, out=self.c1)
+            elif it == 0 and self.raw16:
+                K.asw_vCostAggregation16(p, self.wvl, self.wvr, self.c0_16, out=self.c1, den=self.den_v, den_mode=dmv)
             elif self.vidx:
                 K.aggregate_pass_index(p, DIR_V, self.wvl, self.wvr, self.lut, self.c0, out=self.c1)
             else:

@@ -65,7 +65,9 @@ def tune_variant():
     saved = []
 
     def set_(v):
-        saved.append(_lib.lib().asw_tune_set(1, v))
+        old = _lib.lib().asw_tune_set(1, v)
+        assert old >= 0, f"asw_tune_set rejected pass variant {v:#x} ({old})"  # an unknown bit: never applied
+        saved.append(old)
 
     yield set_
     if saved:

@@ -48,13 +48,6 @@ def main():
     names = ("d_ref", "conf_ref", "d_tar", "conf_tar", "code_ref", "code_tar")
     out["mismatch"] = {n: int((a != getattr(whole, n)).sum()) for a, n in zip(sh, names)}
     out["protocol_equals_wta"] = not any(out["mismatch"].values())
-    if not out["protocol_equals_wta"]:  # diagnostics: the wave-per-pixel variant of the same protocol
-        from stereo_matchin_amd import _lib
-        old = _lib.lib().asw_tune_set(2, 1)
-        sh1 = sharded_wta(HipShardOps(m.p), whole.cost, reduce_min)
-        _lib.lib().asw_tune_set(2, old)
-        out["mismatch_variant1"] = {n: int((a != getattr(whole, n)).sum()) for a, n in zip(sh1, names)}
-        out["mismatch_new_vs_variant1"] = {n: int((a != c).sum()) for a, c, n in zip(sh, sh1, names)}
     dist.destroy_process_group()
     print(json.dumps(out))
 

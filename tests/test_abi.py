@@ -37,9 +37,12 @@ def test_tune_set_rejects_bits_that_select_nothing(L):
     lib = L.lib()
     assert lib.asw_tune_set(1, 64) == L.ASW_E_INVALID      # round 1's 10-wave H form: no longer built
     assert lib.asw_tune_set(1, 1 << 28) == L.ASW_E_INVALID
-    assert lib.asw_tune_set(1, 1 << 26) == 0 and lib.asw_tune_set(1, 0) == 1 << 26  # the minimal lean H32 ring (asw_pass32.h)
-    assert lib.asw_tune_set(1, 1 << 27) == 0 and lib.asw_tune_set(1, 0) == 1 << 27  # k_support's EXPD form
+    assert lib.asw_tune_set(1, 1 << 26) == 0 and lib.asw_tune_set(1, 0) == 1 << 26  # 32-plane passes: nt flipped
+    assert lib.asw_tune_set(1, 1 << 27) == L.ASW_E_INVALID  # (round 5's PD = 2 H form was not kept)
     assert lib.asw_tune_set(2, 5) == L.ASW_E_INVALID
+    # WTA variant 1 (wave per pixel) is no longer built (tools/exp/exp_forms.hip)
+    assert lib.asw_tune_set(2, 1) == L.ASW_E_INVALID
+    assert lib.asw_tune_set(2, 2) == 0 and lib.asw_tune_set(2, 0) == 2
     old = lib.asw_tune_set(1, 128)
     assert lib.asw_tune_set(1, old) == 128
 
@@ -197,13 +200,14 @@ def test_params_flags(L):
     p = L.default_params(32, 32)
     assert p.flags == 0
     for f in (L.FLAG_FUSE_RAW, L.FLAG_SUPPORT_INDEX, L.FLAG_SUPPORT_INDEX_V, L.FLAG_OTF_H, L.FLAG_SHARD_DEN_H,
-              L.FLAG_COMM_LOCAL):
+              L.FLAG_COMM_LOCAL, L.FLAG_RAW_F32, L.FLAG_OTF_V):
         p.flags = f
         assert L.params_check(p) == L.ASW_OK
-    p.flags = 0x40
+    p.flags = 0x100
     assert L.params_check(p) == L.ASW_E_INVALID
     hdr = open(os.path.join(ROOT, "include", "asw.h")).read()
-    for name in ("FUSE_RAW", "SUPPORT_INDEX", "SUPPORT_INDEX_V", "OTF_H", "SHARD_DEN_H", "COMM_LOCAL"):
+    for name in ("FUSE_RAW", "SUPPORT_INDEX", "SUPPORT_INDEX_V", "OTF_H", "SHARD_DEN_H", "COMM_LOCAL", "RAW_F32",
+                 "OTF_V"):
         import re
         v = int(re.search(rf"#define ASW_FLAG_{name} (0x[0-9A-Fa-f]+)", hdr).group(1), 16)
         assert v == getattr(L, f"FLAG_{name}")
@@ -224,3 +228,29 @@ def test_pass_raw_supported(L):
     assert lib.asw_pass_raw_supported(ctypes.byref(shard)) == 0
     from stereo_matchin_amd import kernels as K
     assert K.raw_fused_supported(p) and not K.raw_fused_supported(shard)
+
+
+def test_raw16_supported_and_validation(L):
+    """asw_raw16_supported / asw_raw_cost16 / asw_aggregate_pass_den16 (the uint16 raw
+    costs): integral or absent truncation, ring tap counts, a first pass only; rejected
+    host-side before any launch."""
+    lib = L.lib()
+    ok = L.default_params(64, 32, ndisp=64, taps=35)
+    assert lib.asw_raw16_supported(ctypes.byref(ok)) == 1
+    assert lib.asw_raw16_supported(ctypes.byref(L.default_params(64, 32, ndisp=64, taps=35, tad_tau=40.0))) == 1
+    assert lib.asw_raw16_supported(ctypes.byref(L.default_params(64, 32, ndisp=64, taps=35, tad_tau=40.5))) == 0
+    assert lib.asw_raw16_supported(ctypes.byref(L.default_params(64, 32, ndisp=64, taps=11))) == 0  # no ring kernel
+    assert lib.asw_raw16_supported(ctypes.byref(L.default_params(64, 32, ndisp=64, taps=35, iters=0))) == 0
+    shard = L.default_params(64, 32, ndisp=256, taps=35, d_begin=32, d_end=64)  # pitch 32: k_vpass32
+    assert lib.asw_raw16_supported(ctypes.byref(shard)) == 1
+    x, y = ctypes.c_void_p(1), ctypes.c_void_p(2)
+    frac = L.default_params(64, 32, ndisp=64, taps=35, tad_tau=40.5)
+    assert lib.asw_raw_cost16(ctypes.byref(frac), x, x, y, None) == L.ASW_E_UNSUPPORTED
+    assert lib.asw_raw_cost16(ctypes.byref(ok), None, x, y, None) == L.ASW_E_INVALID
+    # den-read is never a first pass; den-write needs a den volume; in place is refused
+    assert lib.asw_aggregate_pass_den16(ctypes.byref(ok), x, x, x, y, y, L.DEN_READ, None) == L.ASW_E_INVALID
+    assert lib.asw_aggregate_pass_den16(ctypes.byref(ok), x, x, x, y, None, L.DEN_WRITE, None) == L.ASW_E_INVALID
+    assert lib.asw_aggregate_pass_den16(ctypes.byref(ok), x, x, y, y, None, L.DEN_NONE, None) == L.ASW_E_INVALID
+    q = L.default_params(64, 32, ndisp=64, taps=11)
+    assert lib.asw_aggregate_pass_den16(ctypes.byref(q), x, x, x, y, None, L.DEN_NONE, None) == L.ASW_E_UNSUPPORTED
+    assert L.FLAG_RAW_F32 == 0x40

@@ -57,16 +57,16 @@ def test_multi_shard_local_equals_single(gpu, oracle, n):
 
 
 # C4's D = 256 over 8 shards of 32 planes (pitch 32: the half-wave passes), with float
-# supports (default) and index-form supports (asw_params.flags ASW_FLAG_SUPPORT_INDEX /
-# ASW_FLAG_SUPPORT_INDEX_V, read at create)
-@pytest.mark.parametrize("index", ["", "1", "v"])
+# supports (default), index-form supports (asw_params.flags ASW_FLAG_SUPPORT_INDEX /
+# ASW_FLAG_SUPPORT_INDEX_V, read at create) and the V weights on the fly (ASW_FLAG_OTF_V)
+@pytest.mark.parametrize("index", ["", "1", "v", "otfv"])
 def test_multi_shard_d256_eight_way(gpu, index):
     from stereo_matchin_amd import FrameContext, _lib
     Lh, Rh = _pair(7, 96, 320, shift=40)
     p = _p(320, 96, 256, 35, 2)
     with FrameContext(p, devices=[0]) as one:
         ref = one.match(Lh, Rh)
-    p.flags = {"": 0, "1": _lib.FLAG_SUPPORT_INDEX, "v": _lib.FLAG_SUPPORT_INDEX_V}[index]
+    p.flags = {"": 0, "1": _lib.FLAG_SUPPORT_INDEX, "v": _lib.FLAG_SUPPORT_INDEX_V, "otfv": _lib.FLAG_OTF_V}[index]
     with FrameContext(p, devices=[0] * 8) as fc:
         assert [e - b for b, e in fc.shards()] == [32] * 8
         got = fc.match(Lh, Rh)
@@ -203,3 +203,22 @@ def test_graph_mode_equals_eager(gpu):
             b = graphed.match(Lh, Rh, want16=True)
             _same(b, a, KEYS + ("final_rgba", "post_red_rgba", "disp16", "lr16"))
             assert b["timings"]["total"] > 0 and b["timings"]["refine"] > 0
+
+
+# the frame API's raw-cost forms: the uint16 volume (default where asw_raw16_supported)
+# against ASW_FLAG_RAW_F32 (the float volume), whole range and 8 shards of 32 planes,
+# the final volume included
+@pytest.mark.parametrize("devices", [[0], [0] * 8])
+def test_raw16_frame_equals_float(gpu, devices):
+    from stereo_matchin_amd import FrameContext, _lib
+    Lh, Rh = _pair(11, 72, 300, shift=30)
+    p = _p(300, 72, 256, 35, 2)
+    with FrameContext(p, devices=devices) as fc:
+        a = fc.match(Lh, Rh, want_cost=len(devices) == 1)
+    q = p.copy()
+    q.flags = _lib.FLAG_RAW_F32
+    with FrameContext(q, devices=devices) as fc:
+        b = fc.match(Lh, Rh, want_cost=len(devices) == 1)
+    _same(a, b)
+    if len(devices) == 1:
+        assert np.array_equal(a["cost"], b["cost"])

@@ -83,11 +83,8 @@ def test_raw_cost_truncated(gpu, oracle):
 # pair is ragged (W not a multiple of 64, H of 4)
 @pytest.mark.parametrize("T", [1, 3, 5, 17, 33, 35, 41, 51, 57, 65, 71])
 @pytest.mark.parametrize("scene", ["tsukuba", "ragged"])
-@pytest.mark.parametrize("expd", [False, True])  # variant bit 27: k_support computes exp_d itself
-def test_support(gpu, oracle, T, scene, expd, tune_variant):
+def test_support(gpu, oracle, T, scene):
     import stereo_matchin_amd.kernels as K
-    if expd:
-        tune_variant(1 << 27)
     if scene == "tsukuba":
         Lh, Rh, _ = load_scene("tsukuba")
     else:
@@ -210,6 +207,66 @@ def test_raw_fused_first_v_pass(gpu, oracle, T, H, W, D, d0, d1, tau):
     want = oracle.aggregate_pass(sl, sr, cin, T, 0, d0=d0, d1=d1, plane_base=d0)
     got = plane_major(_np(K.asw_vCostAggregation_raw(p, wl, wr, L, R)), d1 - d0)
     assert np.array_equal(got, want)
+
+
+# the raw costs as uint16 (asw_raw_cost16) and the first V pass over them
+# (asw_aggregate_pass_den16, the matcher's and the frame API's default since round 5):
+# the uint16 volume holds exactly asw_raw_cost's floats, and the pass equals the float
+# pass bit for bit (64-lane k_vpass10 and, for a shard of <= 32 planes, k_vpass32),
+# incl. padding planes, truncated AD at an integral tau, both den modes
+@pytest.mark.parametrize("T", [5, 9, 33, 35, 51])
+@pytest.mark.parametrize("H,W,D,d0,d1,tau", [(37, 91, 70, 0, 70, 765.0), (23, 150, 200, 70, 135, 765.0),
+                                              (40, 77, 64, 0, 64, 90.0), (3, 5, 9, 0, 9, 765.0),
+                                              (150, 70, 64, 0, 64, 765.0), (233, 37, 200, 10, 140, 90.0),
+                                              (41, 131, 256, 96, 128, 765.0), (150, 70, 256, 224, 256, 30.0)])
+def test_raw16_first_v_pass(gpu, T, H, W, D, d0, d1, tau):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    Lh, Rh = _rand_pair(T * 3 + W + D, H, W, shift=6)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1, tad_tau=tau)
+    assert K.raw16_supported(p)
+    L, R = _t(Lh, gpu), _t(Rh, gpu)
+    c0 = K.asw_Aggr(p, L, R)
+    c16 = K.asw_Aggr16(p, L, R)
+    assert torch.equal(c16.to(torch.int32).to(torch.float32), c0)  # every plane, the padding zeros too
+    wl, wr = K.asw_vSupport(p, L), K.asw_vSupport(p, R)
+    kern = "k_vpass32_c16<" if K.cost_shape(p)[2] == 32 else "k_vpass10_c16<"
+    for mode in (_lib.DEN_NONE, _lib.DEN_WRITE):
+        den_a = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
+        den_b = den_a.clone()
+        want = K.asw_vCostAggregation(p, wl, wr, c0, den=den_a, den_mode=mode)
+        got = K.asw_vCostAggregation16(p, wl, wr, c16, den=den_b, den_mode=mode)
+        assert K.pass_kernel(0, mode).startswith(kern + f"T={T},"), K.pass_kernel(0, mode)
+        n = d1 - d0
+        assert torch.equal(got[..., :n], want[..., :n]), (mode, torch.nonzero(got[..., :n] != want[..., :n])[:5])
+        if mode == _lib.DEN_WRITE:
+            assert torch.equal(den_b[..., :n], den_a[..., :n])
+
+
+def test_raw16_rejects(gpu):
+    """A non-integral tau truncates the costs to non-integers: no uint16 form
+    (ASW_E_UNSUPPORTED), and the matcher keeps the float volume; den-read is no first pass."""
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    from stereo_matchin_amd.pipeline import StereoMatcher
+    p = _params(40, 16, 64, 9, tad_tau=30.5)
+    assert not K.raw16_supported(p)
+    img = torch.zeros((16, 40, 4), dtype=torch.uint8, device=gpu)
+    with pytest.raises(_lib.AswError) as e:
+        K.asw_Aggr16(p, img, img)
+    assert e.value.status == _lib.ASW_E_UNSUPPORTED
+    assert not StereoMatcher(p, gpu).raw16
+    q = _params(40, 16, 64, 9)
+    assert StereoMatcher(q, gpu).raw16 and not StereoMatcher(_params(40, 16, 64, 9, flags=_lib.FLAG_RAW_F32), gpu).raw16
+    w = K.new_support(q, gpu)
+    c16 = torch.zeros(K.cost_shape(q), dtype=torch.int16, device=gpu)
+    with pytest.raises(_lib.AswError) as e:
+        K.asw_vCostAggregation16(q, w, w, c16, den=K.new_cost(q, gpu), den_mode=_lib.DEN_READ)
+    assert e.value.status == _lib.ASW_E_INVALID
 
 
 # V pass (k_vpass10) on images tall enough for its unclamped interior chunks
@@ -530,9 +587,11 @@ def test_c4_full_frame_oracle_parity(gpu, oracle):
     p, res = _run(gpu, Lh, Rh, D, T, 7, fuse_raw=None)  # the matcher's default (as benched)
     names = _pass_kernels()
     print("C4 pass kernels:", names)
-    fused = StereoMatcher(p, gpu).fuse_raw  # asw_Aggr inside the first V pass (k_vpass10_raw)
+    m = StereoMatcher(p, gpu)
+    fused, raw16 = m.fuse_raw, m.raw16  # the first V pass: k_vpass10_raw (fused) / k_vpass10_c16 (uint16 raw costs)
+    del m
     for dm in (1, 2):
-        v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10"
+        v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10_c16" if raw16 and dm == 1 else "k_vpass10"
         assert names[(0, dm)].startswith(f"{v}<T={T},NW=16,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
         assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW=4,DM={dm}") and names[(1, dm)].endswith(",nt>"), \
             names
@@ -563,9 +622,10 @@ def test_c5_band_oracle_parity(gpu, oracle):
     p, res = _run(gpu, Ls, Rs, D, T, 7, fuse_raw=None, lr_mode=1)
     names = _pass_kernels()
     print("C5 band pass kernels:", names)
-    fused = False  # the matcher's default (p.flags = 0: the two-kernel raw cost + first V pass)
+    from stereo_matchin_amd.kernels import raw16_supported
+    fused, raw16 = False, raw16_supported(p)  # the matcher's default (p.flags = 0): uint16 raw costs
     for dm in (1, 2):
-        v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10"
+        v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10_c16" if raw16 and dm == 1 else "k_vpass10"
         assert names[(0, dm)].startswith(f"{v}<T={T},NW=12,NPH=3,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
         assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW={C5_H_NKW},DM={dm}") and \
             names[(1, dm)].endswith(",nt>"), names

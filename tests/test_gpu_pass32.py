@@ -82,14 +82,50 @@ def test_pass32_bit_exact(gpu, oracle, T, direction, H, W, D, d0, d1):
             assert name.startswith("k_pass_any<"), name
 
 
-# the other H forms behind variant bits (asw_pass32.h): bit 26 = the minimal 40-entry
-# lean ring (the default is the 48-entry one), bit 24 = the 4-wave-block form
+# the V pass with both weights on the fly (asw_aggregate_pass_otf_v): the
+# oracle's pass over its support arrays, bit for bit, for every ring tap count <= 35 on the
+# edge shapes of the float tests, in both cache policies
+@pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35])
+@pytest.mark.parametrize("H,W,D,d0,d1", [(37, 91, 70, 38, 70), (23, 150, 200, 70, 87), (8, 20, 64, 0, 32),
+                                          (9, 331, 256, 224, 256), (150, 70, 256, 96, 128)])
+def test_pass32_otf_v_bit_exact(gpu, oracle, tune_variant, T, H, W, D, d0, d1):
+    import stereo_matchin_amd.kernels as K
+    Lh, Rh = _rand_pair(T * 11 + W, H, W, shift=6)
+    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
+    assert K.otf_v_supported(p)
+    rng = np.random.default_rng(T + D + H + 1)
+    sl, sr = oracle.support(Lh, T, 0), oracle.support(Rh, T, 0)
+    L, R = _t(Lh, gpu), _t(Rh, gpu)
+    lut = K.support_lut(p, gpu)
+    for flip in (False, True):
+        if flip:
+            tune_variant(1 << 26)
+        cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+        want = oracle.aggregate_pass(sl, sr, cin, T, 0, d0=d0, d1=d1, plane_base=d0)
+        out = K.asw_vCostAggregation_otf_v(p, L, R, lut, _t(pixel_major(cin, 32), gpu))
+        assert K.pass_kernel(0, 0).startswith(f"k_vpass32_otf<T={T},"), K.pass_kernel(0, 0)
+        got = plane_major(_np(out), d1 - d0)
+        assert np.array_equal(got, want), (flip, np.argwhere(got != want)[:5])
+
+
+def test_pass32_otf_v_supported_shapes(gpu):
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    assert not K.otf_v_supported(_params(64, 16, 256, 51, d_begin=224, d_end=256))  # T > 35
+    assert not K.otf_v_supported(_params(64, 16, 256, 11, d_begin=224, d_end=256))  # no ring kernel
+    assert not K.otf_v_supported(_params(64, 16, 256, 35, d_begin=192, d_end=256))  # pitch 64
+    assert not K.otf_v_supported(_params(64, 16, 256, 35, d_begin=224, d_end=256, color_space=_lib.COLOR_LAB))
+
+
+# the other forms behind variant bits (asw_pass32.h): bit 26 = the nt cache policy flipped
+# (both passes), bit 24 = the 4-wave-block H form
 @pytest.mark.parametrize("variant", [1 << 26, 1 << 24])
 @pytest.mark.parametrize("T", [9, 35])
 @pytest.mark.parametrize("H,W,D,d0,d1", [(37, 91, 70, 38, 70), (9, 331, 256, 224, 256)])
 def test_pass32_h_variants_bit_exact(gpu, oracle, tune_variant, variant, T, H, W, D, d0, d1):
     tune_variant(variant)
-    test_pass32_bit_exact(gpu, oracle, T, 1, H, W, D, d0, d1)
+    for direction in ((0, 1) if variant == 1 << 26 else (1,)):
+        test_pass32_bit_exact(gpu, oracle, T, direction, H, W, D, d0, d1)
 
 
 def test_pass32_rejects_fused_raw_and_otf(gpu):
@@ -105,6 +141,39 @@ def test_pass32_rejects_fused_raw_and_otf(gpu):
     with pytest.raises(_lib.AswError) as e:
         K.asw_vCostAggregation_raw(p, w, w, img, img, out=x)
     assert e.value.status == _lib.ASW_E_UNSUPPORTED
+
+
+# the full-size C4 shard (1920 x 1080 x 32 x 4 B = 253 MiB, just under the 256 MiB nt
+# threshold) in both cache-policy instantiations of both passes (variant bit 26 flips
+# the policy; ADVICE r04: no smaller test shape reaches the nt ones): one den-none V and
+# one den-none H pass, as the shard's frame runs them, against the oracle over the
+# whole shard
+@pytest.mark.parametrize("flip", [False, True])
+def test_c4_shard_full_size_passes(gpu, oracle, tune_variant, flip):
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    from stereo_matchin_amd.synthetic import make_pair
+    W, H, D, T = 1920, 1080, 256, 35
+    d0, d1 = 96, 128
+    Lh, Rh, _ = make_pair(W, H, D, 5)
+    p = _params(W, H, D, T, iters=7, d_begin=d0, d_end=d1)
+    assert K.cost_shape(p) == (H, W, 32) and H * W * 32 * 4 < 256 << 20
+    if flip:
+        tune_variant(1 << 26)
+    rng = np.random.default_rng(11)
+    cin = (rng.random((d1 - d0, H, W)) * 700).astype(np.float32)
+    for direction in (0, 1):
+        sl, sr = oracle.support(Lh, T, direction), oracle.support(Rh, T, direction)
+        want = oracle.aggregate_pass(sl, sr, cin, T, direction, d0=d0, d1=d1, plane_base=d0)
+        f = K.asw_vSupport if direction == 0 else K.asw_hSupport
+        g = K.asw_vCostAggregation if direction == 0 else K.asw_hCostAggregation
+        out = g(p, f(p, _t(Lh, gpu)), f(p, _t(Rh, gpu)), _t(pixel_major(cin, 32), gpu), den_mode=_lib.DEN_NONE)
+        name = K.pass_kernel(direction, _lib.DEN_NONE)
+        assert name.startswith(("k_vpass32<" if direction == 0 else "k_hpass32<") + f"T={T},") and \
+            name.endswith(",nt>") == flip, name
+        got = plane_major(_np(out), d1 - d0)
+        assert np.array_equal(got, want), (direction, np.argwhere(got != want)[:5])
+        cin = want  # the H pass aggregates the V pass's output, as in the frame
 
 
 # the C4 shard of the 8-way split: one rank's 32 planes of a 1920-column D256 T35
@@ -128,16 +197,19 @@ def test_c4_shard_band_r7(gpu, oracle):
         cost = oracle.aggregate_pass(*sv, cost, T, 0, d0=d0, d1=d1, plane_base=d0)
         cost = oracle.aggregate_pass(*sh, cost, T, 1, d0=d0, d1=d1, plane_base=d0)
     # float supports (the default), index-form supports (opt-in), and
-    # float supports with the H denominators cached (ASW_FLAG_SHARD_DEN_H)
-    for index, denh in ((None, "0"), (True, "0"), (None, "1")):
-        p.flags = _lib.FLAG_SHARD_DEN_H if denh == "1" else 0
+    # float supports with the H denominators cached (ASW_FLAG_SHARD_DEN_H), and the V
+    # weights on the fly (ASW_FLAG_OTF_V: no V support arrays)
+    for index, denh, otfv in ((None, "0", False), (True, "0", False), (None, "1", False), (None, "0", True)):
+        p.flags = (_lib.FLAG_SHARD_DEN_H if denh == "1" else 0) | (_lib.FLAG_OTF_V if otfv else 0)
         m = StereoMatcher(p, gpu, support_index=index)
+        assert m.otfv == otfv and (m.wvl is None) == otfv
         m.raw_and_support(_t(Lb, gpu), _t(Rb, gpu))
         got = plane_major(_np(m.aggregate()), d1 - d0)
         # (a 32-plane shard recomputes the denominators of both directions by default)
         tag = ",IDX" if index else ""
         assert m.vidx == m.hidx == bool(index)
-        assert K.pass_kernel(0, 0).startswith("k_vpass32<T=35,NW=16,NPH=4" + tag), K.pass_kernel(0, 0)
+        assert K.pass_kernel(0, 0).startswith(("k_vpass32_otf" if otfv else "k_vpass32") + "<T=35,NW=16,NPH=4" + tag), \
+            K.pass_kernel(0, 0)
         assert (m.den_h is not None) == (denh == "1")
         assert K.pass_kernel(1, 2 if denh == "1" else 0).startswith(
             "k_hpass32<T=35,NWB=" + ("8,NPH=4,IDX" if index else "1,NPH=4")), K.pass_kernel(1, 0)

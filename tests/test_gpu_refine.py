@@ -128,12 +128,13 @@ def test_frame_api_refine(gpu, oracle):
     assert out["timings"]["refine"] > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 2])
 @pytest.mark.parametrize("H,W,D", [(1, 1, 1), (5, 67, 61), (13, 129, 256), (3, 200, 300), (7, 64, 33),
                                    (2, 700, 128), (4, 1000, 256), (3, 63, 200), (2, 300, 2)])
 def test_wta_variants_on_random_volume(gpu, oracle, variant, H, W, D):
-    """asw_WTA: the lane-per-pixel scan (variant 0), the wave-per-pixel reduction (1) and
-    the row sweep (2: Dp 64 / 128 / 256, the scan elsewhere) against the oracle on
+    """asw_WTA: the lane-per-pixel scan (variant 0) and the row sweep (2: Dp 64 / 128 /
+    256, the scan elsewhere; round 1's wave-per-pixel form is checked by
+    tools/exp/exp_forms.py) against the oracle on
     volumes with many exact ties (rows longer than the 255-plane diagonals, the clamped
     first points of pixels x < md, rows not a multiple of 64 pixels)."""
     import stereo_matchin_amd.kernels as K

@@ -14,7 +14,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-from stereo_matchin_amd import StereoMatcher, make_params  # noqa: E402
+from stereo_matchin_amd import StereoMatcher, _lib, make_params  # noqa: E402
 from stereo_matchin_amd import kernels as K  # noqa: E402
 from stereo_matchin_amd.synthetic import make_pair  # noqa: E402
 
@@ -33,7 +33,7 @@ def main():
     W, H, D, T = (3840, 2160, 512, 51) if args.c5 else (1920, 1080, 256, 35)
     dev = torch.device("cuda:0")
     Lh, Rh, _ = make_pair(W, H, D, 0)
-    p = make_params(W, H, ndisp=D, taps=T, iters=7)
+    p = make_params(W, H, ndisp=D, taps=T, iters=7, flags=_lib.FLAG_RAW_F32)  # c0 = the float raw costs
     m = StereoMatcher(p, dev, otf=False)
     m.raw_and_support(torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev))
     # a realistic H input: one V pass of the raw cost
@@ -54,7 +54,7 @@ def main():
                          ctypes.c_void_p(st.cuda_stream))
         assert rc == 0, rc
 
-    if args.c5:
+    if args.c5 and not args.v:
         # V den-read at T = 51: production pass against k_vpass10 shapes, one library each
         # (--c5libs lib:shape,...; shape = NW*100 + NPH*10 + RB)
         cur = torch.cuda.current_stream().cuda_stream
@@ -114,7 +114,10 @@ def main():
                 "vpx0": ("px0", 2, 0), "vpx4": ("px4", 2, 0), "vpx8": ("px8", 2, 0),
                 "vpx_e": ("px_e", 2, 0), "vpx_f": ("px_f", 2, 0), "vpx_g": ("px_g", 2, 0),
                 # round 4: 8-column blocks at 4 waves per SIMD (two blocks per CU)
-                "vpx_n8w4": ("px_n8w4", 2, 0)}
+                "vpx_n8w4": ("px_n8w4", 2, 0),
+                # round 5: XCD-round tiles of TK plane blocks x 32/TK column groups (libexp_vtile.so)
+                "vtile1": (("tile", 1), 2, 0), "vtile2": (("tile", 2), 2, 0), "vtile4": (("tile", 4), 2, 0),
+                "vtile8": (("tile", 8), 2, 0)}
         vexps = [(n,) + allv[n] for n in args.vexps.split(",")]
         for rep in range(args.reps + 1):
             for name, kind, dm, ns in vexps:
@@ -124,6 +127,11 @@ def main():
                 e0.record()
                 if kind is None:
                     K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=denv if dm else None, den_mode=dm)
+                elif isinstance(kind, tuple):  # k_vpass10 in XCD-round tiles (libexp_vtile.so)
+                    lx = pxlibs.setdefault("tile", ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp_vtile.so")))
+                    rc = lx.exp_vtile(kind[1], pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                    assert rc == 0, rc
                 elif isinstance(kind, str):  # k_vpass10 with extra cost prefetch (libexp_vpx<N>.so)
                     lx = pxlibs.setdefault(kind, ctypes.CDLL(os.path.join(ROOT, "tools", "exp", f"libexp_v{kind}.so")))
                     rc = lx.exp_vpx(dm, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),

@@ -73,10 +73,52 @@ extern "C" int exp_vpx(int dm, const asw_params *p, const float *wl, const float
     const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
     nstrip = (H + rows - 1) / rows;
     const int per_xcd = (nxb + 7) / 8;
-    hipLaunchKernelGGL((k_vpass10<35, VNW, DM_READ, VRB, kCPStream, kCPStream, 2, VPS, false, VNPH, EXP_VPX, VWPE>),
+    hipLaunchKernelGGL((k_vpass10<35, VNW, DM_READ, VRB, kCPStream, kCPStream, 2, VPS, 0, VNPH, EXP_VPX, VWPE>),
                        dim3(8 * per_xcd * nkb * nstrip), dim3(VNW * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp,
                        p->d_begin, rows, nxb, nstrip, per_xcd);
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+#endif
+
+#ifdef EXP_VTILE
+// k_vpass10 den-read in XCD-round tiles (round 5): TK plane blocks x 32/TK column groups
+// per round of 32 blocks, so a round shares its left-weight columns across its plane
+// blocks and a band of right-weight entries.  T = 35 (C4
+// shape, 16 columns) or 51 (C5 shape, 12 columns, 3 phases).
+extern "C" int exp_vtile(int tk, const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                         float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int T = p->taps;
+    if (T != 35 && T != 51) return -4;
+    const int NW = T == 35 ? 16 : 12;
+    const int U = T == 35 ? pf9_period(35) : pf9_period(51);
+    const int W = p->width, H = p->height, Dp = asw_disp_pitch(p), nkb = Dp / 64, nxb = (W + NW - 1) / NW;
+    int nstrip = (int)((2048LL + (long long)nxb * nkb - 1) / ((long long)nxb * nkb));
+    const int max_strip = H / (2 * T) > 1 ? H / (2 * T) : 1;
+    if (nstrip > max_strip) nstrip = max_strip;
+    if (nstrip < 1) nstrip = 1;
+    const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
+    nstrip = (H + rows - 1) / rows;
+    const int per_xcd = (nxb + 7) / 8;
+    auto grid = [&](int TKv) {
+        const int tcg = 32 / TKv;
+        return dim3(8 * 32 * ((nkb + TKv - 1) / TKv) * ((per_xcd + tcg - 1) / tcg) * nstrip);
+    };
+#define VT(TKV)                                                                                                      \
+    if (tk == TKV) {                                                                                                 \
+        if (T == 35)                                                                                                 \
+            hipLaunchKernelGGL((k_vpass10<35, 16, DM_READ, 2, kCPStream, kCPStream, 2, 4, TKV, 2>), grid(TKV),       \
+                               dim3(16 * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp, p->d_begin, rows, nxb, nstrip, \
+                               per_xcd);                                                                             \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_vpass10<51, 12, DM_READ, 2, kCPStream, kCPStream, 2, 4, TKV, 3>), grid(TKV),       \
+                               dim3(12 * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp, p->d_begin, rows, nxb, nstrip, \
+                               per_xcd);                                                                             \
+        return hipGetLastError() == hipSuccess ? 0 : -2;                                                             \
+    }
+    VT(1) VT(2) VT(4) VT(8)
+#undef VT
+    return -4;
 }
 #endif
 
@@ -97,11 +139,11 @@ extern "C" int exp_c5s(int nstrip, int kbi, const asw_params *p, const float *wl
     nstrip = (H + rows - 1) / rows;
     const int per_xcd = (nxb + 7) / 8;
     if (kbi)
-        hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, 2, kCPStream, kCPStream, 2, 4, true, 3>),
+        hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, 2, kCPStream, kCPStream, 2, 4, 4, 3>),
                            dim3(8 * per_xcd * nkb * nstrip), dim3(NW * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp,
                            p->d_begin, rows, nxb, nstrip, per_xcd);
     else
-        hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, 2, kCPStream, kCPStream, 2, 4, false, 3>),
+        hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, 2, kCPStream, kCPStream, 2, 4, 0, 3>),
                            dim3(8 * per_xcd * nkb * nstrip), dim3(NW * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp,
                            p->d_begin, rows, nxb, nstrip, per_xcd);
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -42,7 +42,7 @@ def main():
     D = args.ndisp or D
     dev = torch.device("cuda:0")
     Lh, Rh, _ = make_pair(W, H, D, 0)
-    p = make_params(W, H, ndisp=D, taps=T, iters=iters)
+    p = make_params(W, H, ndisp=D, taps=T, iters=iters, flags=_lib.FLAG_RAW_F32)  # c0 = the float raw costs
     if args.planes:
         p.d_begin, p.d_end = 0, args.planes
     # float supports (materialised whr too: both H forms are timed); a 32-plane shard's V

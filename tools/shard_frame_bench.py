@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--support-index", default="", choices=["", "1", "v"],
                     help="index-form supports (asw_aggregate_pass_index): both directions, or V only (A/B)")
     ap.add_argument("--variants", default="0")
+    ap.add_argument("--flags", default="0",
+                    help="asw_params.flags values (ASW_FLAG_*), timed in turn like the variants, e.g. 0,64 "
+                         "(64 = ASW_FLAG_RAW_F32: the float raw-cost volume)")
     ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
     from stereo_matchin_amd import _lib
@@ -39,10 +42,14 @@ def main():
     W, H, D, T, r = (1920, 1080, 256, 35, 7) if a.workload == "c4" else (3840, 2160, 512, 51, 7)
     Lh, Rh, _ = make_pair(W, H, D, 0)
     L, R = torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev)
-    p = make_params(W, H, ndisp=D, taps=T, iters=r, lr_check=1, lr_mode=1 if D > 256 else 0)
-    m = ShardedStereoMatcher(p, a.rank, a.world, dev, support_index={"": None, "1": True, "v": "v"}[a.support_index])
+    ms_ = {}
+    for f in [int(x) for x in a.flags.split(",")]:
+        p = make_params(W, H, ndisp=D, taps=T, iters=r, lr_check=1, lr_mode=1 if D > 256 else 0, flags=f)
+        ms_[f] = ShardedStereoMatcher(p, a.rank, a.world, dev,
+                                      support_index={"": None, "1": True, "v": "v"}[a.support_index])
     for _ in range(a.rounds):
-        for v in [int(x) for x in a.variants.split(",")]:
+        for v, f in [(int(x), f) for x in a.variants.split(",") for f in ms_]:
+            m = ms_[f]
             old = lib.asw_tune_set(1, v)
             m.match(L, R)
             torch.cuda.synchronize()
@@ -53,7 +60,8 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3 / a.reps
             lib.asw_tune_set(1, old)
             print(json.dumps({"workload": a.workload, "world": a.world, "rank": a.rank,
-                              "planes": m.p.d_stop - m.p.d_begin, "variant": v,
+                              "planes": m.p.d_stop - m.p.d_begin, "variant": v, "flags": f,
+                              "raw16": m.matcher.raw16, "otf_v": m.matcher.otfv,
                               "support_index": {"v": m.matcher.vidx, "h": m.matcher.hidx},
                               "ms_per_shard_frame_no_collective": round(ms, 3)}), flush=True)
 

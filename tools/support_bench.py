@@ -22,8 +22,9 @@ from stereo_matchin_amd.synthetic import make_pair  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,134217728",
-                    help="asw_tune_set(ASW_TUNE_PASS_VARIANT) values; bit 27: k_support computes exp itself")
+    ap.add_argument("--variants", default="0",
+                    help="asw_tune_set(ASW_TUNE_PASS_VARIANT) values (none select a support form since round 5: "
+                         "the EXPD form is tools/exp/exp_forms.hip)")
     ap.add_argument("--c5", action="store_true", help="3840x2160 (default 1920x1080)")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--taps", type=int, default=35)

@@ -88,6 +88,58 @@ __global__ __launch_bounds__(1024) void k_flat_w(const float *a, const float *b,
     }
 }
 
+// Controls: the guide's "float4 copy" (1 read + 1 write, 6.29 TB/s
+// measured by the guide's authors) and a read-only stream, in the same harness, so the
+// 2-read + 1-write rate above is read against the harness's own copy rate.
+template <int VW, int PFW, bool NT>
+__global__ __launch_bounds__(256) void k_copy_w(const float *a, float *o, long long n) {
+    using v_t = float __attribute__((ext_vector_type(VW)));
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    const long long chunks = n / (64 * VW);
+    const v_t *av = reinterpret_cast<const v_t *>(a);
+    v_t *ov = reinterpret_cast<v_t *>(o);
+    for (long long c = wave; c < chunks; c += nw * PFW) {
+        v_t x[PFW];
+#pragma unroll
+        for (int k = 0; k < PFW; ++k) {
+            const long long cc = c + k * nw;
+            if (cc < chunks) x[k] = NT ? __builtin_nontemporal_load(av + cc * 64 + lane) : av[cc * 64 + lane];
+        }
+#pragma unroll
+        for (int k = 0; k < PFW; ++k) {
+            const long long cc = c + k * nw;
+            if (cc < chunks) {
+                if constexpr (NT) __builtin_nontemporal_store(x[k], ov + cc * 64 + lane);
+                else ov[cc * 64 + lane] = x[k];
+            }
+        }
+    }
+}
+
+template <int VW, int PFW>
+__global__ __launch_bounds__(256) void k_read_w(const float *a, float *o, long long n) {
+    using v_t = float __attribute__((ext_vector_type(VW)));
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    const long long chunks = n / (64 * VW);
+    const v_t *av = reinterpret_cast<const v_t *>(a);
+    float acc = 0.0f;
+    for (long long c = wave; c < chunks; c += nw * PFW) {
+        v_t x[PFW];
+#pragma unroll
+        for (int k = 0; k < PFW; ++k) {
+            const long long cc = c + k * nw;
+            x[k] = cc < chunks ? av[cc * 64 + lane] : v_t{};
+        }
+#pragma unroll
+        for (int k = 0; k < PFW; ++k) acc += x[k][0];
+    }
+    if (acc == -1.0f) o[0] = acc;  // never (inputs are 0): keeps the loads
+}
+
 // H pattern with VW planes per lane: a wave covers 64*VW planes of one pixel, the
 // block the Dp/(64 VW) waves of one row segment
 template <int VW>
@@ -242,5 +294,30 @@ int main() {
     time("flat_w16_def", [&] { hipLaunchKernelGGL((k_flat_w<4, 4, false>), dim3(4096), dim3(1024), 0, 0, a, b, o, n); });
     time("flat_w16_g1024", [&] { hipLaunchKernelGGL((k_flat_w<4, 4, true>), dim3(1024), dim3(1024), 0, 0, a, b, o, n); });
     time("flat_w16_g16k", [&] { hipLaunchKernelGGL((k_flat_w<4, 2, true>), dim3(16384), dim3(256), 0, 0, a, b, o, n); });
+    // controls: bytes = 2n*4 (copy) and n*4 (read); "TBps" printed on those bytes
+    auto timeb = [&](const char *name, double nbytes, auto fn) {
+        std::vector<float> ts;
+        for (int r = 0; r < 12; ++r) {
+            hipEventRecord(e0);
+            fn();
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            if (r >= 2) ts.push_back(ms);
+        }
+        std::sort(ts.begin(), ts.end());
+        const float med = ts[ts.size() / 2];
+        std::printf("{\"pattern\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f}\n", name, med, nbytes / med / 1e9);
+    };
+    const double cb = 2.0 * n * 4, rb = 1.0 * n * 4;
+    timeb("copy_f4_g16k_pf2_def", cb, [&] { hipLaunchKernelGGL((k_copy_w<4, 2, false>), dim3(16384), dim3(256), 0, 0, a, o, n); });
+    timeb("copy_f4_g16k_pf4_def", cb, [&] { hipLaunchKernelGGL((k_copy_w<4, 4, false>), dim3(16384), dim3(256), 0, 0, a, o, n); });
+    timeb("copy_f4_g16k_pf2_nt", cb, [&] { hipLaunchKernelGGL((k_copy_w<4, 2, true>), dim3(16384), dim3(256), 0, 0, a, o, n); });
+    timeb("copy_f4_g4k_pf4_def", cb, [&] { hipLaunchKernelGGL((k_copy_w<4, 4, false>), dim3(4096), dim3(256), 0, 0, a, o, n); });
+    timeb("copy_f4_g64k_pf1_def", cb, [&] { hipLaunchKernelGGL((k_copy_w<4, 1, false>), dim3(65536), dim3(256), 0, 0, a, o, n); });
+    timeb("copy_f1_g16k_pf8_def", cb, [&] { hipLaunchKernelGGL((k_copy_w<1, 8, false>), dim3(16384), dim3(256), 0, 0, a, o, n); });
+    timeb("read_f4_g16k_pf4", rb, [&] { hipLaunchKernelGGL((k_read_w<4, 4>), dim3(16384), dim3(256), 0, 0, a, o, n); });
+    timeb("read_f1_g16k_pf8", rb, [&] { hipLaunchKernelGGL((k_read_w<1, 8>), dim3(16384), dim3(256), 0, 0, a, o, n); });
     return 0;
 }
