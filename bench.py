@@ -92,6 +92,9 @@ def parse():
                          "target scan, LR check) on a side stream overlapping frame k+1's aggregation "
                          "(distributed.PipelinedMatcher; stage API).  auto: on for N > 1 (it hides the exchange), "
                          "off on one GPU (measured the same there: 23.63 vs 23.59 ms, profiles/r04/pipeline_r10h.log)")
+    ap.add_argument("--overlap-prep", type=int, default=1,
+                    help="with the pipeline: run frame k+1's raw cost and supports on a third stream beside frame "
+                         "k's passes (distributed.PipelinedMatcher overlap_prep; 0: after them)")
     ap.add_argument("--traffic", default=os.path.join(HERE, "profiles", "traffic.json"))
     ap.add_argument("--flags", type=int, default=0,
                     help="asw_params.flags (ASW_FLAG_*): opt-in forms, e.g. 64 = ASW_FLAG_RAW_F32 (the float "
@@ -306,8 +309,11 @@ def main():
         nloc = D
     else:
         pairs = [(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)) for L, R in pairs_h]
+        torch.cuda.synchronize()  # resident inputs (PipelinedMatcher overlap_prep does not wait for their copy)
         if args.pipeline:
-            m = PipelinedMatcher(p, grank, G, dev, group=pg)
+            # (the pairs are resident and synchronized: the next frame's raw cost and supports
+            # may run beside this frame's passes, overlap_prep)
+            m = PipelinedMatcher(p, grank, G, dev, group=pg, overlap_prep=args.overlap_prep)
             nloc = m.p.d_stop - m.p.d_begin
         elif G > 1:
             m = ShardedStereoMatcher(p, grank, G, dev, group=pg)
@@ -425,7 +431,7 @@ def main():
         subs2 = [dist.new_group(list(range(g * g2, (g + 1) * g2)), backend="gloo" if rehearsal else None)
                  for g in range(world // g2)]
         if args.pipeline:  # (streamed like the main run)
-            m2 = PipelinedMatcher(p, rank % g2, g2, dev, group=subs2[rank // g2])
+            m2 = PipelinedMatcher(p, rank % g2, g2, dev, group=subs2[rank // g2], overlap_prep=args.overlap_prep)
             run2 = m2.submit
         else:
             m2 = ShardedStereoMatcher(p, rank % g2, g2, dev, group=subs2[rank // g2])
@@ -502,7 +508,8 @@ def main():
             "config": {"workload": desc, "width": W, "height": H, "ndisp": D, "taps": T, "iters": iters,
                        "lr_check": lr, "lr_mode": "native" if lr_mode else "u8", "pairs_per_step": batch,
                        "local_planes": nloc, "frames_per_step": groups * batch, "flags": args.flags,
-                       "api": args.api + ("+graph" if frame and args.graph else "") + ("+pipeline" if args.pipeline else ""),
+                       "api": args.api + ("+graph" if frame and args.graph else "") + ("+pipeline" if args.pipeline else "")
+                       + ("+overlap_prep" if args.pipeline and args.overlap_prep else ""),
                        "parallelism": (f"{groups} frame group(s), each d-sharded over {G} GPU(s)"
                                        if world > 1 else "single GPU")},
             "roofline": {"bound": "hbm", "achieved": round(gbs(dom_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -162,8 +162,16 @@ class PipelinedMatcher:
     the ``depth``-th later ``submit`` (the next one into the same set) overwrites it, so
     a caller that needs the volume (e.g. for ``refine``) copies it before then."""
 
-    def __init__(self, params: AswParams, rank: int = 0, world: int = 1, device="cuda", group=None, depth: int = 2):
+    def __init__(self, params: AswParams, rank: int = 0, world: int = 1, device="cuda", group=None, depth: int = 2,
+                 overlap_prep: bool = False):
         self.device = torch.device(device)
+        # overlap_prep: frame k+1's raw cost and support weights (d-independent of frame
+        # k's volumes, in the other set's buffers) run on a third stream while frame k's
+        # passes run, instead of after them on the main stream.  The caller's images must
+        # then be valid when submit() is called (resident inputs, or their producer
+        # synchronized): the preparation does not wait for the caller's stream.
+        self.overlap_prep = overlap_prep
+        self.prep = torch.cuda.Stream(self.device) if overlap_prep else None
         self.sharded = world > 1
         if self.sharded:
             self.sets = [ShardedStereoMatcher(params, rank, world, self.device, group) for _ in range(depth)]
@@ -188,7 +196,20 @@ class PipelinedMatcher:
         if events is not None:
             events.append(("start", _record()))
         fuse = m.fuse_raw and m.p.iters >= 1
-        m.raw_and_support(left, right, raw=not fuse)
+        if self.overlap_prep:
+            # raw cost + supports of this frame on the prep stream, after set i's previous
+            # tail (its last reader), beside whatever the main stream is running
+            if self.done[i] is not None:
+                self.prep.wait_event(self.done[i])
+            with torch.cuda.stream(self.prep):
+                m.raw_and_support(left, right, raw=not fuse)
+                prepared = torch.cuda.Event()
+                prepared.record(self.prep)
+            for t in (left, right):
+                t.record_stream(self.prep)
+            main.wait_event(prepared)
+        else:
+            m.raw_and_support(left, right, raw=not fuse)
         if events is not None:
             events.append(("support", _record()))
         cost = m.aggregate(events, images=(left, right) if fuse else None)
@@ -221,3 +242,5 @@ class PipelinedMatcher:
     def flush(self) -> None:
         """Order the current stream after every submitted frame's tail."""
         torch.cuda.current_stream(self.device).wait_stream(self.side)
+        if self.prep is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.prep)

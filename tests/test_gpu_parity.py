@@ -626,7 +626,9 @@ def test_c5_band_oracle_parity(gpu, oracle):
     fused, raw16 = False, raw16_supported(p)  # the matcher's default (p.flags = 0): uint16 raw costs
     for dm in (1, 2):
         v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10_c16" if raw16 and dm == 1 else "k_vpass10"
-        assert names[(0, dm)].startswith(f"{v}<T={T},NW=12,NPH=3,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
+        # 12-column blocks in 3 phases; on this 3840-wide band in XCD-round tiles of 4 plane
+        # blocks (v12_tiles in asw_aggregate_impl.h)
+        assert names[(0, dm)] == f"{v}<T={T},NW=12,NPH=3,TK=4,DM={dm},nt>", names
         assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW={C5_H_NKW},DM={dm}") and \
             names[(1, dm)].endswith(",nt>"), names
     ref = oracle.match(Ls, Rs, D, T, 7, want_cost=True)

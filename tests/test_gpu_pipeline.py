@@ -26,7 +26,10 @@ def _np(res):
     return {k: getattr(res, k).cpu().numpy() for k in KEYS}
 
 
-def test_pipelined_whole_range_equals_match(gpu):
+# overlap_prep: frame k+1's raw cost and supports on a third stream beside frame k's
+# passes (the inputs are resident and synchronized before the first submit)
+@pytest.mark.parametrize("overlap_prep", [False, True])
+def test_pipelined_whole_range_equals_match(gpu, overlap_prep):
     import torch
 
     from stereo_matchin_amd import StereoMatcher, make_params
@@ -35,7 +38,8 @@ def test_pipelined_whole_range_equals_match(gpu):
     p = make_params(W, H, ndisp=D, taps=T, iters=3)
     pairs = [(torch.from_numpy(L).to(gpu), torch.from_numpy(R).to(gpu)) for L, R in _pairs(5, H, W, D)]
     want = [_np(StereoMatcher(p, gpu).match(L, R)) for L, R in pairs]
-    pm = PipelinedMatcher(p, device=gpu)
+    torch.cuda.synchronize()
+    pm = PipelinedMatcher(p, device=gpu, overlap_prep=overlap_prep)
     got = [pm.submit(L, R) for L, R in pairs]  # 5 frames through 2 sets of volumes
     pm.flush()
     torch.cuda.synchronize()
@@ -45,7 +49,7 @@ def test_pipelined_whole_range_equals_match(gpu):
             assert np.array_equal(g[key], want[k][key]), (k, key)
 
 
-def _rank_main(rank, world, port, out, H, W, D, T):
+def _rank_main(rank, world, port, out, H, W, D, T, overlap_prep=False):
     import torch
     import torch.distributed as dist
 
@@ -55,10 +59,10 @@ def _rank_main(rank, world, port, out, H, W, D, T):
     from stereo_matchin_amd.distributed import PipelinedMatcher
     dev = torch.device("cuda:0")
     p = make_params(W, H, ndisp=D, taps=T, iters=3)
-    pm = PipelinedMatcher(p, rank, world, dev)
-    res = []
-    for L, R in _pairs(4, H, W, D):
-        res.append(pm.submit(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)))
+    pm = PipelinedMatcher(p, rank, world, dev, overlap_prep=overlap_prep)
+    inputs = [(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)) for L, R in _pairs(4, H, W, D)]
+    torch.cuda.synchronize()  # (overlap_prep: the inputs are valid before the first submit)
+    res = [pm.submit(L, R) for L, R in inputs]
     pm.flush()
     torch.cuda.synchronize()
     if rank == 0:
@@ -67,7 +71,8 @@ def _rank_main(rank, world, port, out, H, W, D, T):
     dist.destroy_process_group()
 
 
-def test_pipelined_sharded_two_ranks_equals_match(gpu, tmp_path):
+@pytest.mark.parametrize("overlap_prep", [False, True])
+def test_pipelined_sharded_two_ranks_equals_match(gpu, tmp_path, overlap_prep):
     import socket
 
     import torch
@@ -79,7 +84,7 @@ def test_pipelined_sharded_two_ranks_equals_match(gpu, tmp_path):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     out = str(tmp_path / "pipe.npz")
-    tmp.spawn(_rank_main, args=(2, port, out, H, W, D, T), nprocs=2, join=True, start_method="spawn")
+    tmp.spawn(_rank_main, args=(2, port, out, H, W, D, T, overlap_prep), nprocs=2, join=True, start_method="spawn")
     got = np.load(out)
     p = make_params(W, H, ndisp=D, taps=T, iters=3)
     for k, (L, R) in enumerate(_pairs(4, H, W, D)):

@@ -13,12 +13,8 @@ for l in sys.stdin:
 run 300 shard python3 -u tools/shard_frame_bench.py --world 8 --rank 1 --reps 10 --flags 0,64,128 --rounds 3
 grep '^{' $O/shard.log
 run 300 profshard rocprofv3 --kernel-trace --stats --output-format csv -d $O/profshard -o run -- python3 tools/shard_frame_bench.py --world 8 --rank 1 --reps 5 --flags 0,128
-run 600 vtile_c4 python3 -u tools/exp/exp_bench.py --v --lib none --reps 8 --vexps prod_read,vtile1,vtile2,vtile4,vtile8
-grep '^{\|error' $O/vtile_c4.log
 run 600 bench_c5 python3 -u bench.py --workload c5 --steps 2 --warmup 1 --no-cpu
 run 600 bench_c5_f32 python3 -u bench.py --workload c5 --steps 2 --warmup 1 --no-cpu --flags 64
 grep -h '^{' $O/bench_c5*.log | python3 -c "import sys,json
 for l in sys.stdin:
     d=json.loads(l); print(d['config']['flags'], d['ms_per_step'], d['roofline']['v_write_ms'])"
-run 900 vtile_c5 python3 -u tools/exp/exp_bench.py --c5 --v --lib none --reps 3 --vexps prod_read,vtile4,vtile8,vtile2
-grep '^{\|error' $O/vtile_c5.log

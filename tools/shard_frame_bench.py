@@ -17,7 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from stereo_matchin_amd import make_params  # noqa: E402
-from stereo_matchin_amd.distributed import ShardedStereoMatcher  # noqa: E402
+from stereo_matchin_amd.distributed import PipelinedMatcher, ShardedStereoMatcher  # noqa: E402
 from stereo_matchin_amd.synthetic import make_pair  # noqa: E402
 
 
@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--support-index", default="", choices=["", "1", "v"],
                     help="index-form supports (asw_aggregate_pass_index): both directions, or V only (A/B)")
     ap.add_argument("--variants", default="0")
+    ap.add_argument("--pipeline", default="",
+                    help="also time the frames streamed through distributed.PipelinedMatcher (2 sets of volumes, "
+                         "the tail on a side stream): comma list of overlap_prep values, e.g. 0,1")
     ap.add_argument("--flags", default="0",
                     help="asw_params.flags values (ASW_FLAG_*), timed in turn like the variants, e.g. 0,64 "
                          "(64 = ASW_FLAG_RAW_F32: the float raw-cost volume)")
@@ -64,6 +67,27 @@ def main():
                               "raw16": m.matcher.raw16, "otf_v": m.matcher.otfv,
                               "support_index": {"v": m.matcher.vidx, "h": m.matcher.hidx},
                               "ms_per_shard_frame_no_collective": round(ms, 3)}), flush=True)
+    # streamed frames (what bench.py --gpus N runs per rank), per overlap_prep value
+    for ov in [int(x) for x in a.pipeline.split(",") if x != ""]:
+        p = make_params(W, H, ndisp=D, taps=T, iters=r, lr_check=1, lr_mode=1 if D > 256 else 0)
+        pm = PipelinedMatcher(p, a.rank, a.world, dev, overlap_prep=bool(ov))
+        torch.cuda.synchronize()
+        for _ in range(a.rounds):
+            for _ in range(2):
+                pm.submit(L, R)
+            pm.flush()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.reps):
+                pm.submit(L, R)
+            pm.flush()
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / a.reps
+            print(json.dumps({"workload": a.workload, "world": a.world, "rank": a.rank, "pipelined": True,
+                              "overlap_prep": ov, "planes": pm.p.d_stop - pm.p.d_begin,
+                              "ms_per_shard_frame_no_collective": round(ms, 3)}), flush=True)
+        del pm
+
 
 if __name__ == "__main__":
     main()
