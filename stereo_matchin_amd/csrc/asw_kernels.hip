@@ -79,8 +79,11 @@ __global__ void k_support_lut(float *lut, int rows, float gamma_c, float gamma_g
 // asw_Aggr (K/asw_aggr.cl:3-23): per-disparity absolute-difference cost.
 // Block = 4 waves on row blockIdx.y, 4*PPW consecutive pixels; the right-image
 // pixels they reach (columns x - d) are staged once in LDS, so each lane's four
-// planes d = 4q..4q+3 read LDS instead of four gathers; the left pixel is
-// wave-uniform.  Every store is a float4 per lane (1 KB per wave-instruction).
+// planes d = 4q..4q+3 read LDS instead of four gathers; the wave's 16 left pixels
+// are one load.  The cost |dR|+|dG|+|dB| of 8-bit channels is an integer below 766,
+// so the reference's float sum of three fabs equals v_sad_u8 of the alpha-cleared
+// pixels exactly (one instruction instead of six conversions, three subtractions and
+// two adds).  Every store is a float4 per lane (1 KB per wave-instruction).
 // U16 (asw_raw_cost16): the same costs as uint16 (an integer AD <= 765, or its
 // truncation at an integral tau), a 4 x uint16 store per lane: half the bytes.
 // ---------------------------------------------------------------------------
@@ -96,46 +99,58 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
     // (t >> 2).  The lanes of a read are 4 elements apart (planes 4q..4q+3 of lane q),
     // so they read consecutive dwords of one phase (a linear row: 4-way conflicts), and
     // s4 = 8 (mod 32) spreads the staging writes of 32 consecutive t over 32 banks.
-    extern __shared__ uchar4 rrow[];
+    extern __shared__ unsigned rrow[];
     const int s4 = ((kRawSpan + Dp - 1 + 3) / 4 + 31) / 32 * 32 + 8;
     auto slot = [s4](int t) __attribute__((always_inline)) { return (t & 3) * s4 + (t >> 2); };
     const int y = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uchar4 *Lrow = L + (long long)y * W, *Rrow = R + (long long)y * W;
+    const unsigned *Lrow = reinterpret_cast<const unsigned *>(L + (long long)y * W);
+    const unsigned *Rrow = reinterpret_cast<const unsigned *>(R + (long long)y * W);
     const int x0 = blockIdx.x * kRawSpan;
     const int xlo = x0 - (d_begin + Dp - 1);  // smallest x - d of the block (staged clamped to [0, W-1])
     const int nr = kRawSpan + Dp - 1;
+    // (alpha cleared: v_sad_u8 then sums |dR| + |dG| + |dB|)
     for (int t = threadIdx.x; t < nr; t += 256) {
         const int xr = xlo + t;
-        rrow[slot(t)] = Rrow[xr < 0 ? 0 : (xr >= W ? W - 1 : xr)];
+        rrow[slot(t)] = Rrow[xr < 0 ? 0 : (xr >= W ? W - 1 : xr)] & 0xFFFFFFu;
     }
-    __syncthreads();
-    const int nq = Dp >> 2;
     const int xa = x0 + wave * kRawPPW;
     const int xb = min(xa + kRawPPW, W);
+    // the wave's 16 left pixels in one load (lane i: pixel xa + i), each taken by the
+    // lanes that need it through a lane permute
+    const unsigned lw = Lrow[min(xa + (lane & (kRawPPW - 1)), W - 1)] & 0xFFFFFFu;
+    // an integral tau below 765 clamps the integer cost (the uint16 form's domain,
+    // raw16_exact); the float form clamps the exact float sum, as fminf(sum, tau)
+    const unsigned tau_u = tau >= 765.0f ? 765u : (unsigned)tau;
+    __syncthreads();
+    const int nq = Dp >> 2;
     // Dp < 256 (narrow shards): 64/nq pixels per wave iteration, so no lane idles
     const int ppi = (nq < 64 && 64 % nq == 0) ? 64 / nq : 1;
     const int lpp = ppi > 1 ? nq : 64;  // lanes per pixel
-    for (int x = xa + lane / lpp; x < xb; x += ppi) {
-        const uchar4 l = Lrow[x];
+    // (a uniform trip count: the permute reads lanes that must all be active; Dp is 32
+    // or a multiple of 64, so ppi <= 8 divides kRawPPW)
+    for (int it = 0; it < kRawPPW / ppi; ++it) {
+        const int x = xa + lane / lpp + it * ppi;
+        const unsigned l = (unsigned)__shfl((int)lw, min(x - xa, kRawPPW - 1));
+        if (x >= xb) continue;
         const long long e0 = ((long long)y * W + x) * Dp;  // first element of pixel x
         for (int q = lane % lpp; q < nq; q += lpp) {
-            f4 v;
+            unsigned c[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int k = 4 * q + j;
-                const int d = d_begin + k;
-                const uchar4 r = rrow[slot(x - d - xlo)];  // = R(max(x-d, 0), y): the stage clamps
-                float sv = fabsf((float)l.x - (float)r.x) + fabsf((float)l.y - (float)r.y);
-                sv = sv + fabsf((float)l.z - (float)r.z);
-                v[j] = k < nloc ? fminf(sv, tau) : 0.0f;
+                const unsigned r = rrow[slot(x - (d_begin + k) - xlo)];  // = R(max(x-d, 0), y): the stage clamps
+                c[j] = k < nloc ? __builtin_amdgcn_sad_u8(l, r, 0u) : 0u;  // exact integer AD, <= 765
             }
             if constexpr (U16) {
                 u4 h;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) h[j] = (unsigned short)v[j];  // exact: integers in [0, 765]
+                for (int j = 0; j < 4; ++j) h[j] = (unsigned short)min(c[j], tau_u);
                 reinterpret_cast<u4 *>(static_cast<unsigned short *>(cost_v) + e0)[q] = h;
             } else {
+                f4 v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = 4 * q + j < nloc ? fminf((float)c[j], tau) : 0.0f;
                 reinterpret_cast<f4 *>(static_cast<float *>(cost_v) + e0)[q] = v;
             }
         }
@@ -519,9 +534,10 @@ int asw_tune_set(int key, int value) {
     if (key == ASW_TUNE_PASS_VARIANT) {
         // only bits that select a compiled form (launch_dm): a stale bit would time the
         // default kernel under another name
-        // (+ bits 16-26: strip / segment counts, the H form, the index-form H phases and
-        // the nt policy flip of the 32-plane shard passes, asw_pass32.h)
-        if (value & ~(asw::kPassVariantBits | 0x7FF0000)) return ASW_E_INVALID;
+        // (+ bits 16-27: strip / segment counts, the H form, the index-form H phases, the
+        // nt policy flip and the lean H form's left ring in LDS (the default: DPP rows) of
+        // the 32-plane shard passes, asw_pass32.h)
+        if (value & ~(asw::kPassVariantBits | 0xFFF0000)) return ASW_E_INVALID;
         return asw::set_pass_variant(value);
     }
     if (key == ASW_TUNE_WTA_VARIANT) {

@@ -18,6 +18,12 @@
 //   k_hpass32: a wave holds rows y (h=0) and y+1 (h=1) of one row segment, sweeping
 //              x; its right and left entries live in a wave-private LDS ring per row
 //              (no block barrier: the waves of a block share nothing).
+//              DL: the left entries never enter LDS.  Each lane loads float4 q =
+//              lane & 15 of its row's left entry straight into VGPRs, a window-prefetch
+//              ahead, and tap i takes wl_i from lane i/4 of its 16-lane DPP row
+//              (row_newbcast, the DPP operand of the tap's v_mul_f32: no extra
+//              instruction).  Half the LDS reads of a step, and 13.8 instead of 16.7 KB
+//              of LDS per wave: 11 waves per CU instead of 9.
 #pragma once
 #include <cstdio>
 
@@ -39,6 +45,25 @@ __device__ __forceinline__ void taps32(float &num, float &den, const f4 (&wl)[M]
         num = __builtin_fmaf(ww, win[(S + i) % U], num);
         if constexpr (DEN) den = den + ww;
     }
+}
+
+// DL: value v of lane N of each 16-lane row, as the DPP operand of its user
+template <int N>
+__device__ __forceinline__ float row_bcast(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x150 + N, 0xF, 0xF, true));
+}
+
+// taps [B, E) with the left weights in DPP rows (DL): wl = this lane's float4 of the
+// left entry, tap i's weight in component i % 4 of lane i / 4 of the row
+template <int U, int S, int B, int E, bool DEN, int M>
+__device__ __forceinline__ void taps32_dl(float &num, float &den, const f4 &wl, const f4 (&wr)[M],
+                                          const float (&win)[U]) {
+    static_for<B, E>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        const float ww = row_bcast<i / 4>(wl[i % 4]) * wr[(i - B) / 4][(i - B) % 4];
+        num = __builtin_fmaf(ww, win[(S + i) % U], num);
+        if constexpr (DEN) den = den + ww;
+    });
 }
 
 // ---------------------------------------------------------------------------
@@ -359,7 +384,8 @@ constexpr int h32_batch(int T) { return tap_pitch(T) / 4 * 8 <= 64 * 4 ? 4 : 2; 
 // (Round 5: the weights requested two phases ahead instead of one measured 0.3115
 // against 0.3173 ms per pass and the same shard frame, profiles/r05/pd2_nt_r12c.log;
 // not kept.)
-template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0>
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0,
+          bool DL = false>
 __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_hpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
     float *__restrict__ den, int W, int H, int d_begin, int nseg, int seg_len, int npairs, int pairs_per_xcd,
@@ -372,11 +398,13 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     constexpr int KD = 4;  // den prefetch ring (steps)
     constexpr int K = KB ? KB : h32_batch(T);
     constexpr int RING = RING16 ? (32 + 2 * K + 15) / 16 * 16 : 32 + 2 * K;  // right entries per row
-    constexpr int LRING = 2 * K + 2;                   // left entries per row
+    constexpr int LRING = DL ? 0 : 2 * K + 2;          // left entries per row (not DL)
     constexpr int ROWE = RING + LRING;                 // ring entries per row
     static_assert(U % K == 0, "the batch top must be a compile-time step");
-    // staged per batch: 2 rows x (K right + K left entries) x Q float4 over 64 lanes
-    constexpr int NST = 4 * K * Q;
+    static_assert(!DL || (!IDX && (T + 3) / 4 <= 16), "DL: float supports, taps in one DPP row");
+    // staged per batch: 2 rows x (K right + K left entries, DL: K right) x Q float4 over 64 lanes
+    constexpr int NK = DL ? 1 : 2;
+    constexpr int NST = 2 * NK * K * Q;
     constexpr int SPL = (NST + 63) / 64;  // float4 per lane
     __shared__ f4 ring_all[NWB][2 * ROWE * Q];
     constexpr int NLUT = IDX ? (R + 1) * kLutWidth : 1;
@@ -434,7 +462,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
         const int n = min(j * 64 + lane, NST - 1);
-        const int q = n % Q, k = (n / Q) % K, kind = (n / (Q * K)) & 1, r = n / (2 * Q * K);
+        const int q = n % Q, k = (n / Q) % K, kind = (n / (Q * K)) % NK, r = n / (NK * Q * K);
         st_row[j] = (gelem_t *)(kind == 0 ? wrrows[r] : wlrows[r]);
         st_q4[j] = 4 * q;
         st_k[j] = k;
@@ -443,7 +471,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
         // LDS float4 index of the entry for the first top (xb = xs: entries of batch xs + K)
         const int e = xs + K + 1 + k;
         st_slot[j] = kind == 0 ? (r * ROWE + (e - d0 + (1 << 20)) % RING) * Q + q
-                               : (r * ROWE + RING + e % LRING) * Q + q;
+                               : (r * ROWE + RING + e % (DL ? 1 : LRING)) * Q + q;
         st_base[j] = kind == 0 ? r * ROWE * Q : (r * ROWE + RING) * Q;
     }
     auto st_load = [&](int j, int xb) __attribute__((always_inline)) {  // entry of the batch starting at xb
@@ -452,7 +480,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     };
 
     // the rings before step xs: right entries [xs-d0-31, xs+K-d0], left [xs, xs+K]
-    constexpr int NR0 = 32 + K, NL0 = K + 1;
+    constexpr int NR0 = 32 + K, NL0 = DL ? 0 : K + 1;
     for (int t = lane; t < 2 * (NR0 + NL0) * Q; t += 64) {
         const int q = t % Q, ee = t / Q;
         const int r = ee / (NR0 + NL0), e = ee % (NR0 + NL0);
@@ -493,11 +521,21 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
         if (s >= RING) v = v >= RING ? v - RING : v;  // (s is a compile-time step)
         return myrow + v * Q;
     };
-    auto wl_at = [&](int x) __attribute__((always_inline)) { return myrow + (RING + x % LRING) * Q; };
+    auto wl_at = [&](int x) __attribute__((always_inline)) { return myrow + (RING + x % (DL ? 1 : LRING)) * Q; };
+    // DL: this lane's float4 of its row's left entry at a column (global-address pointer)
+    using gf4 = const __attribute__((address_space(1))) f4;
+    gelem_t *wlsrc = (gelem_t *)(wle + (long long)y * W * TP + 4 * min(lane & 15, Q - 1));
+    auto wl_load = [&](int x) __attribute__((always_inline)) { return *(gf4 *)(wlsrc + min(x, W - 1) * TP); };
+    constexpr int NLD = DL ? ring_div(U, P) : 1;  // left columns in flight (>= the window's P)
+    f4 wld[NLD];
+    if constexpr (DL) {
+#pragma unroll
+        for (int j = 0; j < NLD; ++j) wld[j] = wl_load(xs + j);
+    }
 
     using PH = Phases<T, NPH>;
     float win[U];
-    f4 wlp[NPH][PH::NG], wrp[NPH][PH::NG];
+    f4 wlp[DL ? 1 : NPH][PH::NG], wrp[NPH][PH::NG];
     float dring[KD];
 #pragma unroll
     for (int j = 0; j < U - 1; ++j) win[j] = bload<CP>(rc, voff, clampi(xs - R + j, 0, W - 1) * xstride);
@@ -508,7 +546,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     // weights of phase k at step x = xb + s (rs0: the right slot at xb)
     auto request = [&](auto kc, int x, int rs0, int s) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
-        read_wr<T, PH::gb(k), PH::gb(k + 1)>(wlp[k], wl_at(x));
+        if constexpr (!DL) read_wr<T, PH::gb(k), PH::gb(k + 1)>(wlp[k], wl_at(x));
         read_wr<T, PH::gb(k), PH::gb(k + 1)>(wrp[k], wr_at(rs0, s));
     };
     request(std::integral_constant<int, 0>{}, xs, wr_slot0(xs), 0);
@@ -547,9 +585,11 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
             if constexpr (k + 1 < NPH) request(std::integral_constant<int, k + 1>{}, x, rs0, s);
             else request(std::integral_constant<int, 0>{}, x + 1, rs0, s + 1);
             __builtin_amdgcn_sched_barrier(0);
-            taps32<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wlp[k], wrp[k], win);
+            if constexpr (DL) taps32_dl<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wld[s % NLD], wrp[k], win);
+            else taps32<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wlp[k], wrp[k], win);
             __builtin_amdgcn_sched_barrier(0);
         });
+        if constexpr (DL) wld[s % NLD] = wl_load(x + NLD);  // column x+NLD's left entry
         const int xo = x * xstride;
         if constexpr (DM == DM_READ) {
             dn = dring[s % KD];
@@ -601,7 +641,8 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
                      CP == kCPStream);
 }
 
-template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0>
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0,
+          bool DL = false>
 void launch_h32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
                 hipStream_t st, int seg_len, const float *lut = nullptr) {
     const int W = p->width, H = p->height;
@@ -609,12 +650,14 @@ void launch_h32(const asw_params *p, const float *wl, const float *wr, const flo
     const int npairs = (H + 1) / 2 * nseg;  // work items: (row pair, segment)
     const int per_xcd = (npairs + 7) / 8;
     const int blocks_per_xcd = (per_xcd + NWB - 1) / NWB;
-    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE, IDX, KB>), dim3(8 * blocks_per_xcd), dim3(NWB * 64),
-                       0, st, wl, wr, cin, cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd, lut);
+    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE, IDX, KB, DL>), dim3(8 * blocks_per_xcd),
+                       dim3(NWB * 64), 0, st, wl, wr, cin, cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd,
+                       lut);
     char shape[48];
     std::snprintf(shape, sizeof shape, "NWB=%d,NPH=%d%s", NWB, NPH, IDX ? ",IDX" : "");
     note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T,
-                     IDX ? shape : NPH == 4 ? "NWB=1,NPH=4" : NWB == 4 ? "NWB=4" : "NWB=2", CP == kCPStream);
+                     IDX ? shape : DL ? "NWB=1,NPH=4,DL" : NPH == 4 ? "NWB=1,NPH=4" : NWB == 4 ? "NWB=4" : "NWB=2",
+                     CP == kCPStream);
 }
 
 inline int finish32() {
@@ -654,14 +697,27 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         // (profiles/r04/pass32_h_r09e.log).  Variant
         // bit 24 selects the 4-wave-block form instead.
         const bool lean = T <= 35 && !(g_pass_variant & (1 << 24));
+        // the lean form with its left weights from DPP rows (DL) by default: in the C4 / 8
+        // frame 0.325 against 0.355 ms per pass under rocprofv3, shard frame 4.71-4.74
+        // against 4.74-4.88 ms (round 5, profiles/r05/kernel_stats_r12q_shard8_hdl.csv,
+        // shard_hdl_r12q.log); variant bit 27 selects the left ring in LDS instead
+        const bool dl = lean && !(g_pass_variant & (1 << 27));
         const int pairs = (p->height + 1) / 2;
-        int nseg = (2048 + pairs / 2) / (pairs > 0 ? pairs : 1);  // C4: 4 segments of 480 columns
+        // (DL: the wave slots its LDS admits, 11 per CU against 9 with the left ring;
+        // C4: 5 segments of 384 columns)
+        const int slots = dl ? 256 * 11 : 2048;
+        int nseg = (slots + pairs / 2) / (pairs > 0 ? pairs : 1);  // C4: 4 segments of 480 columns
         if ((g_pass_variant >> 20) & 15) nseg = (g_pass_variant >> 20) & 15;
         if (nseg < 1) nseg = 1;
         int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
         if (seg < 2 * U) seg = 2 * U;
         constexpr int NWB = T > 35 ? 2 : 4;
         if constexpr (T <= 35) {
+            if (dl) {
+                if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+                else launch_h32<T, 1, DM, 0, 4, true, 3, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+                return finish32();
+            }
             if (lean) {
                 // (one-wave blocks with the conflict-free 48-entry ring, 16.7 KB of LDS, 9 per
                 // CU: C4 8-way shard frame 4.73 against 4.81-4.98 ms with the minimal 40-entry

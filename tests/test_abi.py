@@ -38,7 +38,7 @@ def test_tune_set_rejects_bits_that_select_nothing(L):
     assert lib.asw_tune_set(1, 64) == L.ASW_E_INVALID      # round 1's 10-wave H form: no longer built
     assert lib.asw_tune_set(1, 1 << 28) == L.ASW_E_INVALID
     assert lib.asw_tune_set(1, 1 << 26) == 0 and lib.asw_tune_set(1, 0) == 1 << 26  # 32-plane passes: nt flipped
-    assert lib.asw_tune_set(1, 1 << 27) == L.ASW_E_INVALID  # (round 5's PD = 2 H form was not kept)
+    assert lib.asw_tune_set(1, 1 << 27) == 0 and lib.asw_tune_set(1, 0) == 1 << 27  # lean H form: the left ring in LDS
     assert lib.asw_tune_set(2, 5) == L.ASW_E_INVALID
     # WTA variant 1 (wave per pixel) is no longer built (tools/exp/exp_forms.hip)
     assert lib.asw_tune_set(2, 1) == L.ASW_E_INVALID

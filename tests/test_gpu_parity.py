@@ -78,6 +78,32 @@ def test_raw_cost_truncated(gpu, oracle):
     assert np.array_equal(c, np.minimum(oracle.raw_cost(Lh, Rh, 10), np.float32(40.0)))
 
 
+# the alpha byte never enters the cost (K/asw_aggr.cl sums the three colour channels):
+# random alpha in both images, float and uint16 forms, a plain, a truncating and a
+# non-integral tau (float form only), ragged widths and a d-shard
+@pytest.mark.parametrize("W,H,D,d0,d1,tau", [(97, 13, 70, 0, 70, 765.0), (150, 9, 200, 64, 160, 90.0),
+                                             (40, 7, 64, 0, 64, 30.5), (333, 5, 256, 96, 128, 765.0)])
+def test_raw_cost_random_alpha(gpu, oracle, W, H, D, d0, d1, tau):
+    import torch
+
+    import stereo_matchin_amd.kernels as K
+    rng = np.random.default_rng(W + H + D)
+    Lh = rng.integers(0, 256, (H, W, 4), dtype=np.uint8)
+    Rh = np.roll(Lh, -5, axis=1)
+    Rh = np.ascontiguousarray(np.clip(Rh.astype(int) + rng.integers(-40, 41, Rh.shape), 0, 255).astype(np.uint8))
+    p = _params(W, H, D, 5, d_begin=d0, d_end=d1, tad_tau=tau)
+    want = np.minimum(oracle.raw_cost(Lh, Rh, D)[d0:d1], np.float32(tau))
+    L, R = _t(Lh, gpu), _t(Rh, gpu)
+    c = _np(K.asw_Aggr(p, L, R))
+    assert np.array_equal(plane_major(c, d1 - d0), want)
+    assert (c[:, :, d1 - d0:] == 0).all()
+    if K.raw16_supported(p):
+        c16 = K.asw_Aggr16(p, L, R)
+        assert torch.equal(c16.to(torch.int32).to(torch.float32), torch.from_numpy(c).to(gpu))
+    else:
+        assert tau != int(tau)
+
+
 # every unrolled k_support<Q>, Q = Tp/4 (T 1, 3 -> 1; 5 -> 3; 17 -> 5; 33, 35 -> 9; 41 -> 11;
 # 51 -> 13; 57 -> 15; 65 -> 17; Q = 7 runs end to end at T = 25) and T = 71, the generic float4-per-thread kernel past them; the random
 # pair is ragged (W not a multiple of 64, H of 4)

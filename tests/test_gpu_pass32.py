@@ -128,6 +128,24 @@ def test_pass32_h_variants_bit_exact(gpu, oracle, tune_variant, variant, T, H, W
         test_pass32_bit_exact(gpu, oracle, T, direction, H, W, D, d0, d1)
 
 
+# the lean H form's left weights: from DPP rows (DL, the default; T <= 35) and from the
+# LDS ring (variant bit 27): every ring tap count, all den modes, on the edge shapes, in
+# both cache policies; the V pass and T = 51 have one form
+@pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35, 51])
+@pytest.mark.parametrize("lds_left", [False, True])
+def test_pass32_dl_bit_exact(gpu, oracle, tune_variant, T, lds_left):
+    import stereo_matchin_amd.kernels as K
+    from stereo_matchin_amd import _lib
+    for flip in (False, True):
+        tune_variant((1 << 27 if lds_left else 0) | (1 << 26 if flip else 0))
+        for direction in (0, 1):
+            for H, W, D, d0, d1 in ((37, 91, 70, 38, 70), (8, 20, 64, 0, 32), (9, 331, 256, 224, 256),
+                                    (150, 70, 256, 96, 128)):
+                test_pass32_bit_exact(gpu, oracle, T, direction, H, W, D, d0, d1)
+                name = K.pass_kernel(direction, _lib.DEN_READ)
+                assert (",DL" in name) == (direction == 1 and T <= 35 and not lds_left), name
+
+
 def test_pass32_rejects_fused_raw_and_otf(gpu):
     import torch
 
