@@ -186,24 +186,43 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
     __shared__ f4 stg[4][64 * Q];  // per wave: its 64 pixels' Q float4, in output order
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x0 = blockIdx.x * 64;
-    const int y = blockIdx.y * 4 + wv;
-    if (y >= H) return;  // whole wave
+    const int y0 = blockIdx.y * 4;
+    const int y = y0 + wv;
+    const bool live = y < H;  // (a wave past the bottom row still loads and syncs, stores nothing)
     const int x = min(x0 + lane, W - 1);  // lanes past the right edge recompute column W-1, not stored
-    const uchar4 *__restrict__ img = jobs.img[blockIdx.z];
+    const unsigned *__restrict__ img = reinterpret_cast<const unsigned *>(jobs.img[blockIdx.z]);
     const int dir = jobs.dir[blockIdx.z];
     const int R = T / 2;
-    const uchar4 a = img[y * W + x];
-    // all 4Q neighbour loads, then all 4Q LUT gathers, in flight together (chunks of
-    // 3 or 5 groups measured 0.86 / 0.61 ms against 0.49 at C4: latency-bound)
+    // The block's image window, loaded once into LDS (aliasing the staging tile, which
+    // is written only after every wave has read its neighbours): V rows y0-R .. y0+3+R of
+    // its 64 columns, [4Q+3][64]; H columns x0-R .. x0+63+R of its 4 rows, [4][64+4Q-1].
+    // About 10 (V) or 2 (H) coalesced loads per thread instead of 4Q neighbour loads per
+    // lane: the vector-memory pipe is left to the 4Q LUT gathers and the stores.
+    // (Alpha cleared: v_sad_u8 then sums |dR| + |dG| + |dB|, the reference's exact integer.)
+    unsigned *win = reinterpret_cast<unsigned *>(&stg[0][0]);
+    constexpr int NV = (4 * Q + 3) * 64, HW = 64 + 4 * Q - 1, NH = 4 * HW;
+    static_assert(NV <= 4 * 64 * 4 * Q && NH <= 4 * 64 * 4 * Q, "window inside the staging tile");
+    if (dir == ASW_DIR_V) {
+        for (int t = threadIdx.x; t < NV; t += 256)
+            win[t] = img[clampi(y0 - R + (t >> 6), 0, H - 1) * W + min(x0 + (t & 63), W - 1)] & 0xFFFFFFu;
+    } else {
+        for (int t = threadIdx.x; t < NH; t += 256) {
+            const int r = t / HW, c = t - r * HW;
+            win[t] = img[min(y0 + r, H - 1) * W + clampi(x0 - R + c, 0, W - 1)] & 0xFFFFFFu;
+        }
+    }
+    __syncthreads();
+    // centre (x, y) and tap k of this lane: V window row wv + k, H window column lane + k
+    const int wbase = dir == ASW_DIR_V ? wv * 64 + lane : wv * HW + lane;
+    const int wstep = dir == ASW_DIR_V ? 64 : 1;
+    const unsigned a = win[wbase + R * wstep];
     {
         constexpr int NG = Q;
-        uchar4 b[4 * NG];
+        unsigned b[4 * NG];
 #pragma unroll
-        for (int k = 0; k < 4 * NG; ++k) {
-            const int qx = dir == ASW_DIR_V ? x : clampi(x + k - R, 0, W - 1);
-            const int qy = dir == ASW_DIR_V ? clampi(y + k - R, 0, H - 1) : y;
-            b[k] = img[qy * W + qx];
-        }
+        for (int k = 0; k < 4 * NG; ++k) b[k] = win[wbase + k * wstep];
+        __syncthreads();  // every wave holds its neighbours: the tile is the staging tile again
+        if (!live) return;
         if (jobs.idx[blockIdx.z]) {
             // index form: the weight's LUT index instead of the weight (no gathers),
             // four uint16 per 8-B share, transposed through LDS like the weights
@@ -219,7 +238,7 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
                     const int qx = clampi(x + k - R, 0, W - 1);
                     dist = x > qx ? x - qx : qx - x;
                 }
-                const int sad = abs((int)a.x - (int)b[k].x) + abs((int)a.y - (int)b[k].y) + abs((int)a.z - (int)b[k].z);
+                const int sad = (int)__builtin_amdgcn_sad_u8(a, b[k], 0u);
                 const unsigned ix = k < T ? (unsigned)(dist * kLutWidth + sad) : 0u;
                 if (k % 2 == 0) c[k / 4][(k % 4) / 2] = ix;
                 else c[k / 4][(k % 4) / 2] |= ix << 16;
@@ -250,7 +269,7 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
                 const int qx = clampi(x + k - R, 0, W - 1);
                 dist = x > qx ? x - qx : qx - x;
             }
-            const int sad = abs((int)a.x - (int)b[k].x) + abs((int)a.y - (int)b[k].y) + abs((int)a.z - (int)b[k].z);
+            const int sad = (int)__builtin_amdgcn_sad_u8(a, b[k], 0u);
             v[k / 4][k % 4] = k < T ? lut[dist * kLutWidth + sad] : 0.0f;
         }
         // The wave's 64 pixels are one contiguous 64*Q-float4 run of the output:
