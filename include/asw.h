@@ -83,7 +83,9 @@ typedef struct asw_params {
                                         (asw_raw_cost16 + asw_aggregate_pass_den16) is the default    */
 #define ASW_FLAG_OTF_V 0x80          /* 32-plane shards: both V weights on the fly (asw_aggregate_pass_otf_v),
                                         no wvl / wvr arrays                                            */
-#define ASW_FLAG_ALL 0xFF
+#define ASW_FLAG_WTA_FUSED 0x100     /* the WTA's own scan inside the last H pass
+                                        (asw_aggregate_pass_wta_local), no volume re-read for it       */
+#define ASW_FLAG_ALL 0x1FF
 
 void asw_params_default(asw_params *p);
 int asw_params_check(const asw_params *p);
@@ -96,7 +98,8 @@ int asw_last_hip_error(void); /* hipError_t of the last ASW_E_HIP */
  *   1: round 1;  2: asw_outputs.disp16 / lr16, asw_timings.exchange;
  *   3: asw_params.flags (the context options that were environment variables);
  *      asw_raw_cost16 / asw_aggregate_pass_den16 (the uint16 raw-cost volume);
- *      asw_aggregate_pass_otf_v (a shard's V weights on the fly). */
+ *      asw_aggregate_pass_otf_v (a shard's V weights on the fly);
+ *      asw_aggregate_pass_wta_local (the WTA's own scan in the last H pass). */
 #define ASW_ABI_VERSION 3
 int asw_abi_version(void);
 
@@ -262,6 +265,17 @@ int asw_consistency(const asw_params *p, const int32_t *d_ref, const int32_t *d_
  *   asw_wta_finalize.
  * Exact: the result equals asw_wta on the unsharded volume bit for bit. */
 int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m1, float *m2, void *stream);
+/* The last H pass of a frame with asw_wta_local fused (the same pass as
+ * asw_aggregate_pass_den(ASW_DIR_H, ASW_DEN_READ), the same key / m1 / m2 as asw_wta_local
+ * on its output, in one launch: the WTA's own scan does not re-read the volume).  Where
+ * that pass runs one block over every plane: see asw_pass_wta_local_supported (pitch 256
+ * or 128, ring tap counts <= 35); ASW_E_UNSUPPORTED otherwise.  A whole-range frame
+ * then finishes with asw_wta_target_local, asw_wta_second and asw_wta_finalize (the
+ * one-shard case of the protocol above); a shard feeds key / m1 / m2 to it as usual. */
+int asw_aggregate_pass_wta_local(const asw_params *p, const float *supp_left, const float *supp_right,
+                                 const float *cin, float *cout, const float *den, int64_t *key, float *m1, float *m2,
+                                 void *stream);
+int asw_pass_wta_local_supported(const asw_params *p);
 int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *key_ref, int64_t *tkey,
                          float *t1, float *t2, void *stream);
 int asw_wta_second(const asw_params *p, const int64_t *key_global, const int64_t *key_local, const float *m1,

@@ -51,6 +51,7 @@ FLAG_SHARD_DEN_H = 0x10
 FLAG_COMM_LOCAL = 0x20
 FLAG_RAW_F32 = 0x40
 FLAG_OTF_V = 0x80
+FLAG_WTA_FUSED = 0x100
 
 
 class AswLibraryError(RuntimeError):
@@ -163,6 +164,8 @@ SIGNATURES = {
     "asw_wta": (I, [PP, P, P, P, P, P, P, P, P]),
     "asw_consistency": (I, [PP, P, P, P, P, P, P, P, P, P]),
     "asw_wta_local": (I, [PP, P, P, P, P, P]),
+    "asw_aggregate_pass_wta_local": (I, [PP, P, P, P, P, P, P, P, P, P]),
+    "asw_pass_wta_local_supported": (I, [PP]),
     "asw_wta_target_local": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_second": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_finalize": (I, [PP, P, P, P, P, P, P, P, P, P, P, P]),

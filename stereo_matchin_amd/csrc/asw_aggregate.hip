@@ -28,6 +28,9 @@ int launch_pass32_otf_v_t(const asw_params *p, const uint8_t *left, const uint8_
 template <int T>
 int launch_pass32_idx_tm(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
                          const float *cin, float *cout, float *den, int dm, hipStream_t st);
+template <int T>
+int launch_pass_wta_tm(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                       const float *den, const WtaLocalOut &o, hipStream_t st);
 // a shard of <= 32 planes (pitch 32): the half-wave passes of asw_pass32.h
 template <int T>
 int launch_pass32_t(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
@@ -118,6 +121,51 @@ int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, 
         default:  // no ring kernel for this T: the generic pass (the fused raw cost is opt-in, ring kernels only)
             if (raw) return ASW_E_UNSUPPORTED;
             return launch_pass_any(p, dir, wl, wr, cin, cout, den, dm, st);
+    }
+}
+
+int h11_seg_len(int T, int variant) {
+    int U9 = T + 3;  // pf9_period
+    while (U9 % 4) ++U9;
+    return ((variant >> 8) & 15 ? (variant >> 8) & 15 : (240 + U9 / 2) / U9) * U9;
+}
+
+bool h11_selected(const asw_params *p, int variant) {
+    const int seg = h11_seg_len(p->taps, variant);
+    const long long waves11 = (long long)p->height * ((p->width + seg - 1) / seg) * (asw_disp_pitch(p) / 64);
+    return !(variant & 128) && (waves11 >= 8192 || (variant & 4096));  // bit 4096: k_hpass11 at any size
+}
+
+// the den-read H pass with the local WTA scan fused (asw_aggregate_pass_wta_local):
+// where that pass is k_hpass11 with one block over every plane (Dp = 256 or 128), at
+// the ring tap counts <= 35 (4 waves per SIMD)
+bool pass_wta_local_supported(const asw_params *p) {
+    const int Dp = asw_disp_pitch(p);
+    return ring_taps(p->taps) && p->taps <= 35 && (Dp == 256 || Dp == 128) &&
+           h11_selected(p, agg::g_pass_variant);
+}
+
+int launch_pass_wta_local(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                          const float *den, const WtaLocalOut &o, hipStream_t st) {
+    if (const int s = pass_shape_check(p)) return s;
+    if (!pass_wta_local_supported(p)) return ASW_E_UNSUPPORTED;
+#ifdef ASW_DEV_TAPS
+    if (p->taps == ASW_DEV_TAPS) return agg::launch_pass_wta_tm<ASW_DEV_TAPS>(p, wl, wr, cin, cout, den, o, st);
+    return ASW_E_UNSUPPORTED;
+#endif
+    switch (p->taps) {
+#define ASW_CASE(TT) \
+    case TT:         \
+        return agg::launch_pass_wta_tm<TT>(p, wl, wr, cin, cout, den, o, st);
+        ASW_CASE(3)
+        ASW_CASE(5)
+        ASW_CASE(7)
+        ASW_CASE(9)
+        ASW_CASE(15)
+        ASW_CASE(33)
+        ASW_CASE(35)
+#undef ASW_CASE
+        default: return ASW_E_UNSUPPORTED;
     }
 }
 

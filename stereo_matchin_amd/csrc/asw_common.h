@@ -47,10 +47,26 @@ struct OtfSrc {
     const float *lut;
 };
 
+// the local WTA scan fused into the last H pass (asw_aggregate_pass_wta_local): per
+// pixel key = (m1 bits << 32 | first argmin d), INT64_MAX where no plane is below the
+// sentinel, m1 and m2 over the volume's planes: what k_wta_local_scan writes
+struct WtaLocalOut {
+    long long *key;
+    float *m1, *m2;
+};
+
 // one aggregation pass over every local plane (asw_aggregate.hip)
 // den/dm: cached-denominator mode (ASW_DEN_*; den = NULL with ASW_DEN_NONE)
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
                 float *den, int dm, hipStream_t st, const RawSrc *raw = nullptr, const OtfSrc *otf = nullptr);
+// an H den-read pass with the local WTA scan fused (asw_aggregate_pass_wta_local)
+int launch_pass_wta_local(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                          const float *den, const WtaLocalOut &o, hipStream_t st);
+bool pass_wta_local_supported(const asw_params *p);
+// the H pass's k_hpass11 segment length (variant bits 8..11: U-step chunks, else the
+// multiple of U nearest 240) and its choice against k_hpass9 (launch_dm)
+int h11_seg_len(int T, int variant);
+bool h11_selected(const asw_params *p, int variant);
 // the tap counts with ring kernels (the ones asw_aggregate_pass_otf and the fused
 // raw-cost pass support)
 bool ring_taps(int T);

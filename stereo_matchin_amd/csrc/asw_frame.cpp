@@ -45,7 +45,8 @@ struct Shard {
     bool fuse = false; // asw_Aggr fused into the first V pass (asw_aggregate_pass_raw)
     bool raw16 = false; // the raw costs as uint16 in c0 (asw_raw_cost16 + asw_aggregate_pass_den16)
     bool otfv = false;  // a 32-plane shard's V passes compute both weights (wvl / wvr not allocated)
-    // d-sharded WTA (more than one shard in the frame)
+    bool wtaf = false;  // the last H pass runs the WTA's local scan (asw_aggregate_pass_wta_local) into key / m1 / m2
+    // d-sharded WTA (more than one shard in the frame, or the fused local scan)
     int64_t *key = nullptr, *key_g = nullptr, *tkey = nullptr, *tkey_g = nullptr;
     float *m1 = nullptr, *m2 = nullptr, *t1 = nullptr, *t2 = nullptr, *m2_g = nullptr, *t2_g = nullptr;
     ncclComm_t comm = nullptr;
@@ -306,7 +307,14 @@ int alloc_shard(Shard &s, bool sharded) {
         if (!p32) ASWCHK(dev_alloc(&s.den_v, asw_cost_bytes(p)));
         if (!p32 || (p->flags & ASW_FLAG_SHARD_DEN_H)) ASWCHK(dev_alloc(&s.den_h, asw_cost_bytes(p)));
     }
-    if (sharded) {
+    // ASW_FLAG_WTA_FUSED: the WTA's own scan inside the last H pass where that pass is one
+    // k_hpass11 block over every plane (asw_pass_wta_local_supported); bit-identical maps,
+    // measured slower at C4 (the pass 1.87 against 1.45 ms at 3 instead of 4 blocks per
+    // CU, and the separate target scan 0.29 against asw_wta's 0.57 in all: 23.02-23.06
+    // against 22.95 ms)
+    s.wtaf = (p->flags & ASW_FLAG_WTA_FUSED) && !s.otf && !s.hidx && s.den_h && p->iters >= 2 &&
+             asw_pass_wta_local_supported(p) != 0;
+    if (sharded || s.wtaf) {
         ASWCHK(dev_alloc(&s.key, S * 8));
         ASWCHK(dev_alloc(&s.key_g, S * 8));
         ASWCHK(dev_alloc(&s.tkey, S * 8));
@@ -488,10 +496,25 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
             ASWCHK(asw_aggregate_pass_index(p, ASW_DIR_H, reinterpret_cast<const uint16_t *>(s.whl),
                                             reinterpret_cast<const uint16_t *>(s.whr), s.lut, s.c1, s.c0, s.den_h, dm,
                                             st));
+        else if (s.wtaf && it == p->iters - 1)
+            ASWCHK(asw_aggregate_pass_wta_local(p, s.whl, s.whr, s.c1, s.c0, s.den_h, s.key, s.m1, s.m2, st));
         else ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, s.whl, s.whr, s.c1, s.c0, s.den_h, dm, st));
         if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0 + 2 * it + 2], st));
     }
     return ASW_OK;
+}
+
+// The WTA of a one-shard frame: asw_wta, or, when the last pass ran the local scan,
+// the rest of the one-shard protocol (the target scan and the finalize; a single shard's
+// second minima are its own)
+int single_wta(asw_ctx *c) {
+    Shard &s0 = c->sh[0];
+    if (!s0.wtaf)
+        return asw_wta(&s0.p, s0.c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar,
+                       s0.stream);
+    ASWCHK(asw_wta_target_local(&s0.p, s0.c0, s0.key, s0.tkey, s0.t1, s0.t2, s0.stream));
+    return asw_wta_finalize(&s0.p, s0.key, s0.m2, s0.tkey, s0.t2, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar,
+                            c->code_ref, c->code_tar, s0.stream);
 }
 
 // The d-sharded WTA (asw_wta_local protocol, include/asw.h): maps on shard 0.
@@ -500,7 +523,7 @@ int sharded_wta(asw_ctx *c) {
     for (int i = 0; i < c->n; ++i) {
         Shard &s = c->sh[i];
         HIPCHK(hipSetDevice(s.device));
-        ASWCHK(asw_wta_local(&s.p, s.c0, s.key, s.m1, s.m2, s.stream));
+        if (!s.wtaf) ASWCHK(asw_wta_local(&s.p, s.c0, s.key, s.m1, s.m2, s.stream));  // (else: the last pass's)
         HIPCHK(hipMemcpyAsync(s.key_g, s.key, S * 8, hipMemcpyDeviceToDevice, s.stream));
     }
     ASWCHK(allreduce_min<int64_t>(c, b_key_g, ncclInt64));
@@ -602,7 +625,7 @@ int main_work_untimed(asw_ctx *c) {
     Shard &s0 = c->sh[0];
     hipStream_t st = s0.stream;
     ASWCHK(shard_aggregate(c, 0, nullptr, nullptr, 1, 3, false));
-    ASWCHK(asw_wta(&s0.p, s0.c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar, st));
+    ASWCHK(single_wta(c));
     hipLaunchKernelGGL(k_codes_to_rgba, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, (long long)S,
                        c->code_ref, reinterpret_cast<uchar4 *>(c->disp));
     HIPCHK(hipGetLastError());
@@ -674,8 +697,7 @@ int match_one(asw_ctx *c, const uint8_t *left_rgba, const uint8_t *right_rgba, a
         if (c->comm == COMM_NONE) {
             HIPCHK(hipSetDevice(s0.device));
             HIPCHK(hipEventRecord(ev[e_x], st));
-            ASWCHK(asw_wta(&s0.p, s0.c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar,
-                           st));
+            ASWCHK(single_wta(c));
         } else {
             ASWCHK(sharded_wta(c));
             HIPCHK(hipSetDevice(s0.device));

@@ -826,6 +826,20 @@ int asw_aggregate_pass_otf_v(const asw_params *p, const uint8_t *left_rgba, cons
     return asw::launch_pass_otf_v(p, left_rgba, right_rgba, lut, cin, cout, (hipStream_t)stream);
 }
 
+int asw_pass_wta_local_supported(const asw_params *p) {
+    if (!p || asw_params_check(p) != ASW_OK) return 0;
+    return asw::pass_wta_local_supported(p) ? 1 : 0;
+}
+
+int asw_aggregate_pass_wta_local(const asw_params *p, const float *supp_left, const float *supp_right,
+                                 const float *cin, float *cout, const float *den, int64_t *key, float *m1, float *m2,
+                                 void *stream) {
+    ASW_CHECK_PARAMS(p);
+    if (!supp_left || !supp_right || !cin || !cout || !den || !key || !m1 || !m2 || cin == cout) return ASW_E_INVALID;
+    const asw::WtaLocalOut o{reinterpret_cast<long long *>(key), m1, m2};
+    return asw::launch_pass_wta_local(p, supp_left, supp_right, cin, cout, den, o, (hipStream_t)stream);
+}
+
 int asw_pass_index_supported(const asw_params *p, int dir, int den_mode) {
     if (!p || asw_params_check(p) != ASW_OK) return 0;
     return asw::pass_index_supported(p, dir, den_mode) ? 1 : 0;

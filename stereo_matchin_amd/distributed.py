@@ -125,7 +125,8 @@ class ShardedStereoMatcher:
         if events is not None:
             events.append(("support", _record()))
         cost = m.aggregate(events, images=(left, right) if fuse else None)
-        d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = sharded_wta(self.ops, cost, self.reduce_min)
+        # (m.local: the local scan, when the last pass ran it)
+        d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = sharded_wta(self.ops, cost, self.reduce_min, m.local)
         if events is not None:
             events.append(("wta", _record()))
         lr = red = None
@@ -213,7 +214,9 @@ class PipelinedMatcher:
         if events is not None:
             events.append(("support", _record()))
         cost = m.aggregate(events, images=(left, right) if fuse else None)
-        local = st.ops.local(cost) if self.sharded else None
+        local = m.local  # the local scan, when the last pass ran it (wta_fused)
+        if local is None and self.sharded:
+            local = st.ops.local(cost)
         ready = torch.cuda.Event()
         ready.record(main)
         p = m.p
@@ -223,6 +226,8 @@ class PipelinedMatcher:
                 t.record_stream(self.side)
             if self.sharded:
                 d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = sharded_wta(st.ops, cost, st.reduce_min, local)
+            elif local is not None:
+                d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.wta_from_local(p, cost, *local)
             else:
                 d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.asw_WTA(p, cost)
             lr = red = None

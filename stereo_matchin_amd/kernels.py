@@ -352,6 +352,45 @@ def asw_hCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None,
     return _pass(p, DIR_H, supp_left, supp_right, cost_in, out, den, den_mode)
 
 
+def wta_local_fused_supported(p: AswParams) -> bool:
+    """asw_pass_wta_local_supported: the den-read H pass of this context can run the
+    WTA's own scan fused (asw_aggregate_pass_wta_local)."""
+    return bool(_lib.lib().asw_pass_wta_local_supported(ctypes.byref(p)))
+
+
+def asw_hCostAggregation_wta_local(p: AswParams, supp_left, supp_right, cost_in, den, out=None, key=None, m1=None,
+                                   m2=None):
+    """The last horizontal pass, den-read, with the local WTA scan fused
+    (asw_aggregate_pass_wta_local): ``out`` is asw_hCostAggregation's output and
+    ``(key, m1, m2)`` equal :func:`wta_local` on it.  Returns ``(out, key, m1, m2)``."""
+    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
+    _expect(den, cost_shape(p), torch.float32, "den")
+    _expect(supp_left, support_shape(p), torch.float32, "supp_left")
+    _expect(supp_right, support_shape(p), torch.float32, "supp_right")
+    dev = cost_in.device
+    H, W = p.height, p.width
+    out = new_cost(p, dev) if out is None else out
+    key = torch.empty((H, W), dtype=torch.int64, device=dev) if key is None else key
+    m1 = torch.empty((H, W), dtype=torch.float32, device=dev) if m1 is None else m1
+    m2 = torch.empty((H, W), dtype=torch.float32, device=dev) if m2 is None else m2
+    _expect(out, cost_shape(p), torch.float32, "out")
+    _expect(key, (H, W), torch.int64, "key")
+    _expect(m1, (H, W), torch.float32, "m1")
+    _expect(m2, (H, W), torch.float32, "m2")
+    _lib.check(_lib.lib().asw_aggregate_pass_wta_local(ctypes.byref(p), _ptr(supp_left), _ptr(supp_right),
+                                                       _ptr(cost_in), _ptr(out), _ptr(den), _ptr(key), _ptr(m1),
+                                                       _ptr(m2), _stream(dev)), "asw_aggregate_pass_wta_local")
+    return out, key, m1, m2
+
+
+def wta_from_local(p: AswParams, cost, key, m1, m2):
+    """asw_WTA's outputs on a whole-range volume from its local scan (key, m1, m2; e.g. of
+    asw_hCostAggregation_wta_local): the one-shard case of the d-sharded protocol, the
+    target scan and the finalize (one shard's second minima are its own)."""
+    tkey, t1, t2 = wta_target_local(p, cost, key)
+    return wta_finalize(p, key, m2, tkey, t2)
+
+
 def asw_WTA(p: AswParams, cost: torch.Tensor):
     """Winner-take-all + target map (K/asw_wta.cl:12-82).
 

@@ -49,7 +49,8 @@ class StereoMatcher:
     other r-1 (ASW_DEN_*); bit-identical results, 2 more cost-sized buffers."""
 
     def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool | None = None,
-                 otf: bool | None = None, support_index: bool | str | None = None, otf_v: bool | None = None):
+                 otf: bool | None = None, support_index: bool | str | None = None, otf_v: bool | None = None,
+                 wta_fused: bool | None = None):
         st = _lib.params_check(params)
         if st != _lib.ASW_OK:
             raise _lib.AswError(st, "asw_params_check")
@@ -120,6 +121,22 @@ class StereoMatcher:
                 self.den_v = K.new_cost(self.p, dev)
             if not p32 or params.flags & _lib.FLAG_SHARD_DEN_H:
                 self.den_h = K.new_cost(self.p, dev)
+        # wta_fused: the WTA's own scan runs inside the last H pass (asw_aggregate_pass_wta_local:
+        # a den-read k_hpass11 with one block over every plane), so the WTA does not re-read
+        # the volume for it; aggregate() leaves the scan's key / m1 / m2 in self.local, and
+        # match() / the sharded protocol take them from there.  Bit-identical, measured
+        # slower at C4 (23.02-23.06 against 22.95 ms: the fused pass runs at 3 blocks per CU,
+        # profiles/r05/bench_f1_r12t.log), so opt-in: default (None) params.flags &
+        # ASW_FLAG_WTA_FUSED, as asw_create reads it
+        if wta_fused is None:
+            wta_fused = bool(params.flags & _lib.FLAG_WTA_FUSED)
+        self.wta_fused = (bool(wta_fused) and not self.otf and not self.hidx and self.den_h is not None
+                          and self.p.iters >= 2 and K.wta_local_fused_supported(self.p))
+        H, W = self.p.height, self.p.width
+        self.local = None
+        self._local_bufs = (torch.empty((H, W), dtype=torch.int64, device=dev),
+                            torch.empty((H, W), dtype=torch.float32, device=dev),
+                            torch.empty((H, W), dtype=torch.float32, device=dev)) if self.wta_fused else None
 
     # -- stages ---------------------------------------------------------------
     def raw_and_support(self, left: torch.Tensor, right: torch.Tensor, raw: bool = True):
@@ -149,8 +166,10 @@ class StereoMatcher:
     def aggregate(self, events: list | None = None, images: tuple | None = None):
         """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515).
         ``images`` = (left, right): the first V pass computes the raw cost itself
-        (asw_aggregate_pass_raw) and c0's input content is not used."""
+        (asw_aggregate_pass_raw) and c0's input content is not used.  With ``wta_fused``
+        the last H pass also leaves the WTA's local scan of c0 in ``self.local``."""
         p = self.p
+        self.local = None
         for it in range(p.iters):
             dmv = _lib.DEN_NONE if self.den_v is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
             dm = _lib.DEN_NONE if self.den_h is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
@@ -173,6 +192,10 @@ class StereoMatcher:
             elif self.hidx:
                 K.aggregate_pass_index(p, DIR_H, self.whl, self.whr, self.lut, self.c1, out=self.c0, den=self.den_h,
                                        den_mode=dm)
+            elif self.wta_fused and it == p.iters - 1:
+                key, m1, m2 = self._local_bufs
+                self.local = K.asw_hCostAggregation_wta_local(p, self.whl, self.whr, self.c1, self.den_h, out=self.c0,
+                                                              key=key, m1=m1, m2=m2)[1:]
             else:
                 K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0, den=self.den_h, den_mode=dm)
             if events is not None:
@@ -189,7 +212,10 @@ class StereoMatcher:
         if events is not None:
             events.append(("support", _record()))
         cost = self.aggregate(events, images=(left, right) if fuse else None)
-        d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.asw_WTA(p, cost)
+        if self.local is not None:  # the own scan ran in the last pass: the target scan and finalize
+            d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.wta_from_local(p, cost, *self.local)
+        else:
+            d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.asw_WTA(p, cost)
         if events is not None:
             events.append(("wta", _record()))
         lr = red = None

@@ -200,14 +200,14 @@ def test_params_flags(L):
     p = L.default_params(32, 32)
     assert p.flags == 0
     for f in (L.FLAG_FUSE_RAW, L.FLAG_SUPPORT_INDEX, L.FLAG_SUPPORT_INDEX_V, L.FLAG_OTF_H, L.FLAG_SHARD_DEN_H,
-              L.FLAG_COMM_LOCAL, L.FLAG_RAW_F32, L.FLAG_OTF_V):
+              L.FLAG_COMM_LOCAL, L.FLAG_RAW_F32, L.FLAG_OTF_V, L.FLAG_WTA_FUSED):
         p.flags = f
         assert L.params_check(p) == L.ASW_OK
-    p.flags = 0x100
+    p.flags = 0x200
     assert L.params_check(p) == L.ASW_E_INVALID
     hdr = open(os.path.join(ROOT, "include", "asw.h")).read()
     for name in ("FUSE_RAW", "SUPPORT_INDEX", "SUPPORT_INDEX_V", "OTF_H", "SHARD_DEN_H", "COMM_LOCAL", "RAW_F32",
-                 "OTF_V"):
+                 "OTF_V", "WTA_FUSED"):
         import re
         v = int(re.search(rf"#define ASW_FLAG_{name} (0x[0-9A-Fa-f]+)", hdr).group(1), 16)
         assert v == getattr(L, f"FLAG_{name}")
@@ -228,6 +228,26 @@ def test_pass_raw_supported(L):
     assert lib.asw_pass_raw_supported(ctypes.byref(shard)) == 0
     from stereo_matchin_amd import kernels as K
     assert K.raw_fused_supported(p) and not K.raw_fused_supported(shard)
+
+
+def test_pass_wta_local_supported(L):
+    """asw_pass_wta_local_supported: the local WTA scan fuses into the den-read H pass
+    where that pass is one k_hpass11 block over every plane (pitch 256 or 128, ring tap
+    counts <= 35, a frame large enough for k_hpass11)."""
+    lib = L.lib()
+    q = lambda **kw: lib.asw_pass_wta_local_supported(ctypes.byref(L.default_params(**kw)))  # noqa: E731
+    assert q(width=1920, height=1080, ndisp=256, taps=35) == 1                 # C4
+    assert q(width=1920, height=1080, ndisp=256, taps=35, d_begin=0, d_end=128) == 1  # a 2-way shard
+    assert q(width=1920, height=1080, ndisp=256, taps=51) == 0                 # T > 35
+    assert q(width=3840, height=2160, ndisp=512, taps=35) == 0                 # pitch 512
+    assert q(width=1920, height=1080, ndisp=256, taps=35, d_begin=0, d_end=32) == 0  # pitch 32
+    assert q(width=1920, height=1080, ndisp=256, taps=11) == 0                 # no ring kernel
+    assert q(width=64, height=32, ndisp=256, taps=35) == 0                     # small: k_hpass9
+    old = lib.asw_tune_set(1, 4096)  # k_hpass11 at any size
+    try:
+        assert q(width=64, height=32, ndisp=256, taps=35) == 1
+    finally:
+        lib.asw_tune_set(1, old)
 
 
 def test_raw16_supported_and_validation(L):

@@ -205,6 +205,28 @@ def test_graph_mode_equals_eager(gpu):
             assert b["timings"]["total"] > 0 and b["timings"]["refine"] > 0
 
 
+# (two shards of 128 planes: each fuses its local scan; the exchange takes it from there)
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_wta_fused_frame_equals_default(gpu, tune_variant, devices):
+    """ASW_FLAG_WTA_FUSED (the WTA's own scan in the last H pass, asw_aggregate_pass_wta_local)
+    through asw_match: the same maps and volume as the default frame, one shard (the
+    one-shard protocol's target scan + finalize) and several (the fused key / m1 / m2 into
+    the exchange)."""
+    from stereo_matchin_amd import FrameContext, _lib
+    tune_variant(4096)  # k_hpass11 at any size: the fused form at this test's size
+    Lh, Rh = _pair(13, 72, 300, shift=30)
+    p = _p(300, 72, 256, 35, 3)
+    with FrameContext(p, devices=devices) as fc:
+        a = fc.match(Lh, Rh, want_cost=len(devices) == 1)
+    q = p.copy()
+    q.flags = _lib.FLAG_WTA_FUSED
+    with FrameContext(q, devices=devices) as fc:
+        b = fc.match(Lh, Rh, want_cost=len(devices) == 1)
+    _same(a, b)
+    if len(devices) == 1:
+        assert np.array_equal(a["cost"], b["cost"])
+
+
 # the frame API's raw-cost forms: the uint16 volume (default where asw_raw16_supported)
 # against ASW_FLAG_RAW_F32 (the float volume), whole range and 8 shards of 32 planes,
 # the final volume included
