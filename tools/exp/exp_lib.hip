@@ -149,3 +149,30 @@ extern "C" int exp_c5s(int nstrip, int kbi, const asw_params *p, const float *wl
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
+
+#ifdef EXP_H32
+// k_hpass32 (C4 8-way shard, T = 35, DL left weights) occupancy (round 5, VERDICT r04
+// item 2): the shipped form keeps the conflict-free 48-entry right ring (13.5 KB of LDS
+// per wave: 11 waves per CU; 138 VGPRs would admit 12).  The minimal 40-entry ring
+// (11.25 KB: 14 by LDS) with 3 or 4 waves per SIMD requested: form 0 = shipped (48, WPE 3),
+// 1 = ring 40 / WPE 3, 2 = ring 40 / WPE 4, 3 = ring 48 / WPE 4.  nseg: segments per
+// row pair (the work items; 0 = the shipped 256 x 11 wave-slot rule).
+#include "asw_pass32.h"
+extern "C" int exp_h32(int form, int nseg, int dm, const asw_params *p, const float *wl, const float *wr,
+                       const float *cin, float *cout, float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (p->taps != 35 || dm != DM_NONE) return -4;
+    constexpr int T = 35, U = pf9_period(35);
+    const int pairs = (p->height + 1) / 2;
+    const int slots = form == 0 ? 256 * 11 : form == 3 ? 256 * 11 : 256 * (form == 1 ? 12 : 14);
+    if (nseg <= 0) nseg = (slots + pairs / 2) / (pairs > 0 ? pairs : 1);
+    int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
+    if (seg < 2 * U) seg = 2 * U;
+    if (form == 0) launch_h32<T, 1, DM_NONE, 0, 4, true, 3, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    else if (form == 1) launch_h32<T, 1, DM_NONE, 0, 4, false, 3, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    else if (form == 2) launch_h32<T, 1, DM_NONE, 0, 4, false, 4, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    else if (form == 3) launch_h32<T, 1, DM_NONE, 0, 4, true, 4, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    else return -4;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+#endif
