@@ -10,7 +10,6 @@ unsharded WTA (oracle_wta, pinned to the reference in test_oracle_golden.py)
 bit for bit, on volumes built with many exact ties and with NaN-free zero gaps.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -105,9 +104,8 @@ def _volume(D, H, W, seed):
     return C
 
 
-def _worker(rank, world, port, D, H, W, seed, out_path):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store, D, H, W, seed, out_path):
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     try:
         C = _volume(D, H, W, seed)  # plane-major [D][H][W]
         b, e = shard_range(D, rank, world)
@@ -124,10 +122,9 @@ def _worker(rank, world, port, D, H, W, seed, out_path):
         dist.destroy_process_group()
 
 
-def _group_worker(rank, world, G, port, D, H, W, out_dir):
+def _group_worker(rank, world, G, store, D, H, W, out_dir):
     """bench.py's layout: world/G frame groups, each d-sharded over its G ranks."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     try:
         groups, gid, grank = world // G, rank // G, rank % G
         subs = [dist.new_group(list(range(g * G, (g + 1) * G))) for g in range(groups)]
@@ -160,7 +157,7 @@ def test_frame_groups_gloo(oracle, tmp_path, world, G):
     if not G:
         G = plan_groups(D, world, min_planes=8)
         assert G == 2
-    mp.start_processes(_group_worker, args=(world, G, _free_port(), D, H, W, str(tmp_path)), nprocs=world,
+    mp.start_processes(_group_worker, args=(world, G, _store(tmp_path), D, H, W, str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")
     for gid in range(world // G):
         got = np.load(tmp_path / f"g{gid}.npz")
@@ -177,17 +174,17 @@ def test_plan_groups():
     assert plan_groups(256, 3) == 3 and plan_groups(100, 3) == 1 and plan_groups(256, 6) == 2
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _store(tmp_path):
+    """A FileStore rendezvous file in the test's own directory: no TCP port to pick, so
+    concurrent tests (pytest -n) cannot race for one."""
+    return str(tmp_path / "rendezvous")
 
 
 @pytest.mark.parametrize("world,D,H,W", [(2, 16, 6, 20), (3, 13, 5, 17), (2, 61, 4, 70), (8, 64, 4, 40)])
 def test_sharded_wta_gloo_matches_oracle(oracle, tmp_path, world, D, H, W):
     seed = 1234 + world + D
     out = str(tmp_path / "res.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), D, H, W, seed, out), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _store(tmp_path), D, H, W, seed, out), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(out)
     dr, cr, dt, ct = oracle.wta(_volume(D, H, W, seed))
