@@ -7,7 +7,6 @@ plain StereoMatcher's (itself bit-exact against the oracle, test_gpu_parity.py),
 whole-range matcher and for a 2-rank d-sharded one (gloo over one GPU, as bench.py's
 rehearsal).
 """
-import os
 
 import numpy as np
 import pytest
@@ -49,12 +48,12 @@ def test_pipelined_whole_range_equals_match(gpu, overlap_prep):
             assert np.array_equal(g[key], want[k][key]), (k, key)
 
 
-def _rank_main(rank, world, port, out, H, W, D, T, overlap_prep=False):
+def _rank_main(rank, world, store, out, H, W, D, T, overlap_prep=False):
     import torch
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a FileStore rendezvous in the test's directory: no TCP port to pick (no race under pytest -n)
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     from stereo_matchin_amd import make_params
     from stereo_matchin_amd.distributed import PipelinedMatcher
     dev = torch.device("cuda:0")
@@ -73,18 +72,13 @@ def _rank_main(rank, world, port, out, H, W, D, T, overlap_prep=False):
 
 @pytest.mark.parametrize("overlap_prep", [False, True])
 def test_pipelined_sharded_two_ranks_equals_match(gpu, tmp_path, overlap_prep):
-    import socket
-
     import torch
     import torch.multiprocessing as tmp
 
     from stereo_matchin_amd import StereoMatcher, make_params
     H, W, D, T = 64, 256, 64, 9
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     out = str(tmp_path / "pipe.npz")
-    tmp.spawn(_rank_main, args=(2, port, out, H, W, D, T, overlap_prep), nprocs=2, join=True, start_method="spawn")
+    tmp.spawn(_rank_main, args=(2, str(tmp_path / "rendezvous"), out, H, W, D, T, overlap_prep), nprocs=2, join=True, start_method="spawn")
     got = np.load(out)
     p = make_params(W, H, ndisp=D, taps=T, iters=3)
     for k, (L, R) in enumerate(_pairs(4, H, W, D)):

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--c5libs", default="libexp_c5_1641.so:1641")
     ap.add_argument("--vexps", default="prod_read,v12_read,prod_none")
     ap.add_argument("--h", action="store_true", help="H-pass experiments")
+    ap.add_argument("--vprobe", default="", help="V resource probes dm:probe,... (libexp_vprobe.so)")
+    ap.add_argument("--vdma", default="", help="LDS-DMA V pass forms f,... (libexp_vdma.so)")
     args = ap.parse_args()
     W, H, D, T = (3840, 2160, 512, 51) if args.c5 else (1920, 1080, 256, 35)
     dev = torch.device("cuda:0")
@@ -97,6 +99,86 @@ def main():
                     res.setdefault(name, []).append(e0.elapsed_time(e1))
         for name, ts in res.items():
             print(json.dumps({"exp": name, "ms_median": round(float(np.median(ts)), 4)}), flush=True)
+        return
+    if args.vdma:
+        # the LDS-DMA-staged V pass (asw_vdma.h) against the production pass, every den mode:
+        # bit-exact outputs (and den-write's den), then median times
+        lx = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp_vdma.so"))
+        denv = torch.empty_like(cin)
+        refv = torch.empty_like(cin)
+        K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=refv, den=denv, den_mode=1)
+        denw = torch.empty_like(cin)
+        torch.cuda.synchronize()
+        forms = [int(f) for f in args.vdma.split(",")]
+        cases = [("prod", dm, None) for dm in (0, 1, 2)] + [(f"vdma{f}", dm, f) for f in forms for dm in (0, 1, 2)]
+        res = {}
+        for rep in range(args.reps + 1):
+            for name, dm, f in cases:
+                out.zero_()
+                torch.cuda.synchronize()
+                dbuf = denw if dm == 1 else denv
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                if f is None:
+                    K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=dbuf if dm else None, den_mode=dm)
+                else:
+                    rc = lx.exp_vdma(f, dm, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(dbuf),
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                    assert rc == 0, (name, dm, rc)
+                e1.record()
+                torch.cuda.synchronize()
+                if rep == 0:
+                    ok = bool(torch.equal(out, refv)) and (dm != 1 or bool(torch.equal(denw, denv)))
+                    rec = {"exp": name, "dm": dm, "bit_exact": ok}
+                    if not ok:
+                        bad = (out != refv).nonzero()
+                        rec.update(n=int(bad.shape[0]), first=bad[:4].tolist())
+                    print(json.dumps(rec), flush=True)
+                else:
+                    res.setdefault((name, dm), []).append(e0.elapsed_time(e1))
+        for (name, dm), ts in res.items():
+            print(json.dumps({"exp": name, "dm": dm, "ms_median": round(float(np.median(ts)), 4),
+                              "ms_min": round(min(ts), 4)}), flush=True)
+        return
+    if args.vprobe:
+        # k_vpass10 resource probes (asw_vprobe.h): probe 0 must equal the production pass,
+        # the others are timed only
+        lx = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp_vprobe.so"))
+        denv = torch.empty_like(cin)
+        refv = torch.empty_like(cin)
+        K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=refv, den=denv, den_mode=1)
+        torch.cuda.synchronize()
+        # "dm:probe" (k_vprobe) or "kd:N" (the den-read pass with an N-row den prefetch ring)
+        cases = [("prod", 0, None), ("prod", 2, None)]
+        for x in args.vprobe.split(","):
+            a, b = x.split(":")
+            cases.append((f"kd{b}", 2, -int(b)) if a == "kd" else (f"probe{b}", int(a), int(b)))
+        res = {}
+        for rep in range(args.reps + 1):
+            for name, dm, pr in cases:
+                out.zero_()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                if pr is None:
+                    K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out, den=denv if dm else None, den_mode=dm)
+                elif pr < 0:
+                    rc = lx.exp_vkd(-pr, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
+                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                    assert rc == 0, (name, rc)
+                else:
+                    rc = lx.exp_vprobe(pr, dm, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), P(denv),
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                    assert rc == 0, (name, dm, rc)
+                e1.record()
+                torch.cuda.synchronize()
+                if rep == 0 and (pr is None or pr <= 0):
+                    print(json.dumps({"exp": name, "dm": dm, "bit_exact": bool(torch.equal(out, refv))}), flush=True)
+                elif rep:
+                    res.setdefault((name, dm), []).append(e0.elapsed_time(e1))
+        for (name, dm), ts in res.items():
+            print(json.dumps({"exp": name, "dm": dm, "ms_median": round(float(np.median(ts)), 4),
+                              "ms_min": round(min(ts), 4)}), flush=True)
         return
     # V pass experiments: the production den-write pass gives den_v, the production
     # den-read pass the reference output

@@ -176,3 +176,67 @@ extern "C" int exp_h32(int form, int nseg, int dm, const asw_params *p, const fl
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
+
+#ifdef EXP_VPROBE
+// k_vpass10 resource probes (round 6, asw_vprobe.h): probe 0 is bit-exact, every other
+// probe removes one resource and is wrong by design (timed only)
+#include "asw_vprobe.h"
+extern "C" int exp_vprobe(int probe, int dm, const asw_params *p, const float *wl, const float *wr, const float *cin,
+                          float *cout, float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (p->taps != 35) return -4;
+#define VP(DMV, PR)                                                                                                  \
+    if (dm == DMV && probe == PR) {                                                                                  \
+        launch_vprobe<35, DMV, PR>(p, wl, wr, cin, cout, den, st);                                                  \
+        return hipGetLastError() == hipSuccess ? 0 : -2;                                                             \
+    }
+    VP(0, 0) VP(0, 3) VP(0, 15) VP(0, 16) VP(0, 32) VP(0, 47) VP(0, 19) VP(0, 8)
+    VP(2, 0) VP(2, 67) VP(2, 16) VP(2, 32)
+#undef VP
+    return -4;
+}
+// the production den-read V pass with a deeper den prefetch ring (KDV rows; 2 ships)
+extern "C" int exp_vkd(int kd, const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                       float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (p->taps != 35) return -4;
+    constexpr int U = pf9_period(35);
+    const int W = p->width, H = p->height, Dp = asw_disp_pitch(p), nkb = Dp / 64, nxb = (W + 15) / 16;
+    int nstrip = (int)((2048LL + (long long)nxb * nkb - 1) / ((long long)nxb * nkb));
+    const int max_strip = H / 70 > 1 ? H / 70 : 1;
+    if (nstrip > max_strip) nstrip = max_strip;
+    if (nstrip < 1) nstrip = 1;
+    const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
+    nstrip = (H + rows - 1) / rows;
+    const int per_xcd = (nxb + 7) / 8;
+#define VK(KDV)                                                                                                      \
+    if (kd == KDV) {                                                                                                 \
+        hipLaunchKernelGGL((k_vpass10<35, 16, DM_READ, 2, kCPStream, kCPStream, KDV>), dim3(8 * per_xcd * nkb * nstrip), \
+                           dim3(1024), 0, st, wl, wr, cin, cout, den, W, H, Dp, p->d_begin, rows, nxb, nstrip, per_xcd); \
+        return hipGetLastError() == hipSuccess ? 0 : -2;                                                             \
+    }
+    VK(4) VK(5) VK(8)
+#undef VK
+    return -4;
+}
+#endif
+
+#ifdef EXP_VDMA
+// the LDS-DMA-staged V pass (round 6, asw_vdma.h), every den mode; form = LEADS * 10 + NBUF / 2
+#include "asw_vdma.h"
+extern "C" int exp_vdma(int form, int dm, const asw_params *p, const float *wl, const float *wr, const float *cin,
+                        float *cout, float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (p->taps != 35) return -4;
+#define VD(F, LE, NB)                                                                                                \
+    if (form == F) {                                                                                                 \
+        if (dm == 0) launch_vdma<35, DM_NONE, LE, 2, NB>(p, wl, wr, cin, cout, den, st);                             \
+        else if (dm == 1) launch_vdma<35, DM_WRITE, LE, 2, NB>(p, wl, wr, cin, cout, den, st);                       \
+        else launch_vdma<35, DM_READ, LE, 2, NB>(p, wl, wr, cin, cout, den, st);                                     \
+        return hipGetLastError() == hipSuccess ? 0 : -2;                                                             \
+    }
+    VD(64, 6, 8)
+#undef VD
+    return -4;
+}
+#endif
