@@ -371,13 +371,6 @@ def main():
     # the frame_groups run below launches other ones
     from stereo_matchin_amd import _lib
     ran = {(d, dm): ran_kernel(d, dm) for d in (0, 1) for dm in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ)}
-    # the WTA's own scan fused into the last H pass (asw_aggregate_pass_wta_local): the
-    # stage matcher's choice, or the frame context's (the same support query)
-    if frame:
-        from stereo_matchin_amd import kernels as K
-        wta_fused = bool(args.flags & _lib.FLAG_WTA_FUSED) and iters >= 2 and K.wta_local_fused_supported(p)
-    else:
-        wta_fused = bool(base_matcher(m).wta_fused)
     # per-launch aggregation-pass durations from the events around each pass, classified
     # by the den mode the pass ran: with cached denominators iteration 0 writes them
     # (DEN_WRITE) and iterations 1..r-1 read them; a 32-plane shard runs DEN_NONE throughout
@@ -407,9 +400,7 @@ def main():
                 if name == "refine":
                     refine_ms.append(dict(ev)["consistency"].elapsed_time(e))
                 if name in ("v", "h"):
-                    # (the last H pass with the WTA's own scan fused: its own kind, "h_wl")
-                    kind = ("h", "wl") if name == "h" and bm.wta_fused and it["h"] == iters - 1 else \
-                        (name, pass_den_mode(bm, name, it[name]))
+                    kind = (name, pass_den_mode(bm, name, it[name]))
                     per_kind.setdefault(kind, []).append(prev.elapsed_time(e))
                     it[name] += 1
                     prev = e
@@ -425,10 +416,7 @@ def main():
             e[0].record()
             K.asw_vCostAggregation(m.p, m.wvl, m.wvr, m.c0, out=m.c1)
             e[1].record()
-            if m.otf:
-                K.asw_hCostAggregation_otf(m.p, m.whl, m.right, m.lut, m.c1, out=m.c0)
-            else:
-                K.asw_hCostAggregation(m.p, m.whl, m.whr, m.c1, out=m.c0)
+            K.asw_hCostAggregation(m.p, m.whl, m.whr, m.c1, out=m.c0)
             e[2].record()
             torch.cuda.synchronize()
             v_none.append(e[0].elapsed_time(e[1]))
@@ -472,7 +460,7 @@ def main():
                                 "(the most maps/s on N GPUs; not the headline layout)"}
         del m2
     # max over ranks of every per-kind mean (absent kinds: -1) and of the launches per frame
-    kinds = [(n, dm) for n in ("v", "h") for dm in (_lib.DEN_READ, _lib.DEN_WRITE, _lib.DEN_NONE)] + [("h", "wl")]
+    kinds = [(n, dm) for n in ("v", "h") for dm in (_lib.DEN_READ, _lib.DEN_WRITE, _lib.DEN_NONE)]
     nframes = max(len(frame_ms), 1) if not frame else max(len(per_pass), 1)
     all_pass = [x for xs in per_kind.values() for x in xs]
     vals = [elapsed, float(np.mean(all_pass)) if all_pass else -1.0, float(np.sum(frame_ms))]
@@ -519,8 +507,7 @@ def main():
                        "lr_check": lr, "lr_mode": "native" if lr_mode else "u8", "pairs_per_step": batch,
                        "local_planes": nloc, "frames_per_step": groups * batch, "flags": args.flags,
                        "api": args.api + ("+graph" if frame and args.graph else "") + ("+pipeline" if args.pipeline else "")
-                       + ("+overlap_prep" if args.pipeline and args.overlap_prep else "")
-                       + ("+wta_fused" if wta_fused else ""),
+                       + ("+overlap_prep" if args.pipeline and args.overlap_prep else ""),
                        "parallelism": (f"{groups} frame group(s), each d-sharded over {G} GPU(s)"
                                        if world > 1 else "single GPU")},
             "roofline": {"bound": "hbm", "achieved": round(gbs(dom_ms), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -533,7 +520,6 @@ def main():
                          "v_read_ms": opt(("v", _lib.DEN_READ)), "v_read_frac": optf(("v", _lib.DEN_READ)),
                          "h_read_ms": opt(("h", _lib.DEN_READ)), "h_read_frac": optf(("h", _lib.DEN_READ)),
                          "v_write_ms": opt(("v", _lib.DEN_WRITE)), "h_write_ms": opt(("h", _lib.DEN_WRITE)),
-                         "h_read_wta_scan_ms": opt(("h", "wl")),
                          "v_none_ms": opt(("v", _lib.DEN_NONE)) if in_frame_none else
                          (round(float(np.median(v_none)), 4) if v_none else None),
                          "v_none_frac": optf(("v", _lib.DEN_NONE)) if in_frame_none else
@@ -542,10 +528,8 @@ def main():
                          (round(float(np.median(h_none)), 4) if h_none else None),
                          "h_none_frac": optf(("h", _lib.DEN_NONE)) if in_frame_none else
                          (round(gbs(float(np.median(h_none))) / HBM_PEAK_GBS, 4) if h_none else None),
-                         "kernels_ran": {**{f"{'VH'[d]} {DM_LABEL[dm]}": ran[(d, dm)][0]
-                                            for (n, dm) in kind_ms if dm != "wl" for d in [0 if n == "v" else 1]},
-                                         **({"H den-read, last pass": "k_hpass11_wl (the WTA's own scan fused)"}
-                                            if ("h", "wl") in kind_ms else {})},
+                         "kernels_ran": {f"{'VH'[d]} {DM_LABEL[dm]}": ran[(d, dm)][0]
+                                         for (n, dm) in kind_ms for d in [0 if n == "v" else 1]},
                          "den_modes": ("the frame's passes run den-none (a 32-plane shard keeps no denominator "
                                        "volumes): v/h_none are those passes, timed inside the timed region"
                                        if in_frame_none else

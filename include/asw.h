@@ -68,24 +68,15 @@ typedef struct asw_params {
     int flags;           /* ASW_FLAG_*: frame-API context options (0 = the default forms) */
 } asw_params;
 
-/* asw_params.flags: forms a context (asw_create*) allocates and runs instead of the
- * default ones.  Every form is bit-identical to the default; each was measured slower
- * on MI355X where it is built and is kept opt-in.  A flag whose form is not
- * built for the shape is ignored (the default form runs).  The stage API ignores flags;
- * asw_params_check rejects unknown bits. */
-#define ASW_FLAG_FUSE_RAW 0x1        /* asw_Aggr fused into the first V pass (asw_aggregate_pass_raw)     */
-#define ASW_FLAG_SUPPORT_INDEX 0x2   /* 32-plane shards: index-form supports, both directions            */
-#define ASW_FLAG_SUPPORT_INDEX_V 0x4 /* 32-plane shards: index-form supports, the V passes only          */
-#define ASW_FLAG_OTF_H 0x8           /* right H weights on the fly (asw_aggregate_pass_otf), no whr array */
-#define ASW_FLAG_SHARD_DEN_H 0x10    /* 32-plane shards: cache the H denominators (den-write / den-read) */
+/* asw_params.flags: context options of the frame API (asw_create*).  Every option is
+ * bit-identical to the default; asw_params_check rejects unknown bits.  (Round 6 removed
+ * the opt-in forms that measured slower in every shape; their bits
+ * 0x1, 0x2, 0x4, 0x8, 0x10, 0x80 and 0x100 are no longer accepted.)  The stage API
+ * ignores flags. */
 #define ASW_FLAG_COMM_LOCAL 0x20     /* asw_create_multi: the device-local exchange even for distinct ids */
 #define ASW_FLAG_RAW_F32 0x40        /* keep the float raw-cost volume (asw_raw_cost) where the uint16 one
                                         (asw_raw_cost16 + asw_aggregate_pass_den16) is the default    */
-#define ASW_FLAG_OTF_V 0x80          /* 32-plane shards: both V weights on the fly (asw_aggregate_pass_otf_v),
-                                        no wvl / wvr arrays                                            */
-#define ASW_FLAG_WTA_FUSED 0x100     /* the WTA's own scan inside the last H pass
-                                        (asw_aggregate_pass_wta_local), no volume re-read for it       */
-#define ASW_FLAG_ALL 0x1FF
+#define ASW_FLAG_ALL 0x60
 
 void asw_params_default(asw_params *p);
 int asw_params_check(const asw_params *p);
@@ -98,9 +89,9 @@ int asw_last_hip_error(void); /* hipError_t of the last ASW_E_HIP */
  *   1: round 1;  2: asw_outputs.disp16 / lr16, asw_timings.exchange;
  *   3: asw_params.flags (the context options that were environment variables);
  *      asw_raw_cost16 / asw_aggregate_pass_den16 (the uint16 raw-cost volume);
- *      asw_aggregate_pass_otf_v (a shard's V weights on the fly);
- *      asw_aggregate_pass_wta_local (the WTA's own scan in the last H pass). */
-#define ASW_ABI_VERSION 3
+ *   4: the measured-negative forms removed with their entry points and flags
+ *      (on-the-fly, index-form and fused-raw passes, the fused WTA scan). */
+#define ASW_ABI_VERSION 4
 int asw_abi_version(void);
 
 /* layout helpers */
@@ -142,9 +133,7 @@ int asw_support(const asw_params *p, int dir, const uint8_t *img_rgba, const flo
                 void *stream);
 
 /* the four support arrays of a frame in one launch (asw_vSupport and asw_hSupport of
- * both images, main.cpp:469-484): bit-identical to four asw_support calls.  Any of
- * the four outputs may be NULL (not computed; e.g. whr when the H passes compute it
- * on the fly, asw_aggregate_pass_otf), at least one must be given. */
+ * both images, main.cpp:469-484): bit-identical to four asw_support calls. */
 int asw_support_all(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba, const float *lut,
                     float *wvl, float *whl, float *wvr, float *whr, void *stream);
 
@@ -177,63 +166,6 @@ int asw_aggregate_pass(const asw_params *p, int dir, const float *wl, const floa
 int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin,
                            float *cout, float *den, int den_mode, void *stream);
 
-/* The H pass (asw_hCostAggregation, K/asw_hcost_aggregation.cl:12-44) with the RIGHT
- * support weights computed on the fly: instead of reading the
- * asw_hSupport array of the right image (K/asw_hsupport.cl:19-27, main.cpp:482-484),
- * the pass computes each weight from `right_rgba` (device RGBA8) and the support LUT
- * (asw_support_lut) as asw_support does, so that array is never written nor read.
- * Bit-identical to asw_aggregate_pass_den with wr = asw_support(H, right).  H only,
- * RGB contexts, tap counts with ring kernels (3, 5, 7, 9, 15, 33, 35, 51), not a
- * 32-plane shard (asw_disp_pitch 32; see asw_pass_otf_supported): ASW_E_UNSUPPORTED
- * otherwise. */
-int asw_aggregate_pass_otf(const asw_params *p, int dir, const float *wl, const uint8_t *right_rgba,
-                           const float *lut, const float *cin, float *cout, float *den, int den_mode, void *stream);
-/* 1 when asw_aggregate_pass_otf supports (p, dir), else 0 */
-int asw_pass_otf_supported(const asw_params *p, int dir);
-
-/* The V pass (asw_vCostAggregation, K/asw_vcost_aggregation.cl:11-44) of a 32-plane
- * shard (asw_disp_pitch 32) with BOTH support weights computed on the fly (SURVEY
- * §8(f)3): each weight of the left and right pixels' vertical windows is computed from
- * the device RGBA8 images and the support LUT as asw_support does (K/asw_vsupport.cl:
- * 19-26), so the two asw_vSupport arrays (main.cpp:469-476) are never written nor read.
- * Den mode NONE (a shard's V passes recompute den).  Bit-identical to
- * asw_aggregate_pass_den(V, asw_support(V, left), asw_support(V, right), ..., NONE).
- * RGB contexts, ring tap counts <= 35: see asw_pass_otf_v_supported. */
-int asw_aggregate_pass_otf_v(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba,
-                             const float *lut, const float *cin, float *cout, void *stream);
-int asw_pass_otf_v_supported(const asw_params *p);
-
-/* The first V pass of main.cpp:494-500 with asw_Aggr (main.cpp:463-466,
- * K/asw_aggr.cl:3-23) fused: each window element's raw AD/TAD cost is computed
- * from the two RGBA8 images (device pointers) instead of read from a raw-cost
- * volume, so that volume is never written nor read.  cout (and den per den_mode)
- * are bit-identical to asw_raw_cost followed by asw_aggregate_pass_den(V).  Ring tap
- * counts, not a 32-plane shard: ASW_E_UNSUPPORTED otherwise. */
-int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
-                           const uint8_t *right_rgba, float *cout, float *den, int den_mode, void *stream);
-/* 1 when asw_aggregate_pass_raw is built for p (and p->iters >= 1), else 0 */
-int asw_pass_raw_supported(const asw_params *p);
-
-/* ---- support arrays in INDEX form (the support stream of a d-shard) ----
- * A pass reads its direction's two support arrays, 8*T*S bytes, whatever its plane
- * count: as many bytes as the cost stream of a 32-plane shard (the C4 frame over 8
- * GPUs).  In index form, element (y,x,i) is the LUT index dist*766 + SAD of the weight
- * asw_support writes there (0 in padding taps i >= taps): uint16 [H][W][Tp], half the
- * bytes, and lut[index] (asw_support_lut) is that weight bit for bit.
- * asw_support_all_fmt: asw_support_all with a format per array, bit j of index_mask
- * (j = 0 wvl, 1 whl, 2 wvr, 3 whr) set = that array in index form (a uint16_t *), else
- * float weights.  Index form needs (R+1)*766 <= 65536 and Tp <= 68 (ASW_E_UNSUPPORTED).
- * asw_aggregate_pass_index: asw_aggregate_pass_den reading index-form supports and the
- * LUT, bit-identical to it on the float arrays; built where asw_pass_index_supported
- * (p, dir, den_mode) says 1 (32-plane shards, RGB, ring tap counts <= 35, the V pass
- * with ASW_DEN_NONE, which is what such a shard's frame runs); ASW_E_UNSUPPORTED else. */
-size_t asw_support_index_bytes(const asw_params *p); /* H*W*Tp*2 */
-int asw_support_all_fmt(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba, const float *lut,
-                        void *wvl, void *whl, void *wvr, void *whr, int index_mask, void *stream);
-int asw_aggregate_pass_index(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
-                             const float *cin, float *cout, float *den, int den_mode, void *stream);
-int asw_pass_index_supported(const asw_params *p, int dir, int den_mode);
-
 /* r x (V,H) ping-pong of main.cpp:486-515 on two caller buffers; the result
  * ends in `c0` (c0 holds the raw cost on entry, c1 is scratch). */
 int asw_aggregate(const asw_params *p, const float *wvl, const float *wvr, const float *whl, const float *whr,
@@ -265,17 +197,6 @@ int asw_consistency(const asw_params *p, const int32_t *d_ref, const int32_t *d_
  *   asw_wta_finalize.
  * Exact: the result equals asw_wta on the unsharded volume bit for bit. */
 int asw_wta_local(const asw_params *p, const float *cost, int64_t *key, float *m1, float *m2, void *stream);
-/* The last H pass of a frame with asw_wta_local fused (the same pass as
- * asw_aggregate_pass_den(ASW_DIR_H, ASW_DEN_READ), the same key / m1 / m2 as asw_wta_local
- * on its output, in one launch: the WTA's own scan does not re-read the volume).  Where
- * that pass runs one block over every plane: see asw_pass_wta_local_supported (pitch 256
- * or 128, ring tap counts <= 35); ASW_E_UNSUPPORTED otherwise.  A whole-range frame
- * then finishes with asw_wta_target_local, asw_wta_second and asw_wta_finalize (the
- * one-shard case of the protocol above); a shard feeds key / m1 / m2 to it as usual. */
-int asw_aggregate_pass_wta_local(const asw_params *p, const float *supp_left, const float *supp_right,
-                                 const float *cin, float *cout, const float *den, int64_t *key, float *m1, float *m2,
-                                 void *stream);
-int asw_pass_wta_local_supported(const asw_params *p);
 int asw_wta_target_local(const asw_params *p, const float *cost, const int64_t *key_ref, int64_t *tkey,
                          float *t1, float *t2, void *stream);
 int asw_wta_second(const asw_params *p, const int64_t *key_global, const int64_t *key_local, const float *m1,

@@ -33,7 +33,7 @@ DISP16_INVALID = 0xFFFF
 COMM_ID_BYTES = 128
 # the asw_outputs / asw_timings layouts mirrored below (ASW_ABI_VERSION of include/asw.h):
 # a library of another revision would write past them, so _load() refuses it
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 DIR_V = 0
 DIR_H = 1
@@ -42,16 +42,9 @@ COLOR_RGB = 0
 COLOR_LAB = 1
 LR_U8 = 0
 LR_NATIVE = 1
-# asw_params.flags (ASW_FLAG_*): frame-API context options, the opt-in forms
-FLAG_FUSE_RAW = 0x1
-FLAG_SUPPORT_INDEX = 0x2
-FLAG_SUPPORT_INDEX_V = 0x4
-FLAG_OTF_H = 0x8
-FLAG_SHARD_DEN_H = 0x10
+# asw_params.flags (ASW_FLAG_*): frame-API context options (ABI 4)
 FLAG_COMM_LOCAL = 0x20
 FLAG_RAW_F32 = 0x40
-FLAG_OTF_V = 0x80
-FLAG_WTA_FUSED = 0x100
 
 
 class AswLibraryError(RuntimeError):
@@ -146,26 +139,14 @@ SIGNATURES = {
     "asw_support_lab": (I, [PP, I, P, P, P]),
     "asw_aggregate_pass": (I, [PP, I, P, P, P, P, P]),
     "asw_aggregate_pass_den": (I, [PP, I, P, P, P, P, P, I, P]),
-    "asw_aggregate_pass_raw": (I, [PP, P, P, P, P, P, P, I, P]),
-    "asw_aggregate_pass_otf": (I, [PP, I, P, P, P, P, P, P, I, P]),
-    "asw_pass_otf_supported": (I, [PP, I]),
-    "asw_aggregate_pass_otf_v": (I, [PP, P, P, P, P, P, P]),
-    "asw_pass_otf_v_supported": (I, [PP]),
-    "asw_pass_raw_supported": (I, [PP]),
     "asw_raw_cost16": (I, [PP, P, P, P, P]),
     "asw_aggregate_pass_den16": (I, [PP, P, P, P, P, P, I, P]),
     "asw_raw16_supported": (I, [PP]),
-    "asw_support_index_bytes": (ctypes.c_size_t, [PP]),
-    "asw_support_all_fmt": (I, [PP, P, P, P, P, P, P, P, I, P]),
-    "asw_aggregate_pass_index": (I, [PP, I, P, P, P, P, P, P, I, P]),
-    "asw_pass_index_supported": (I, [PP, I, I]),
     "asw_aggregate": (I, [PP, P, P, P, P, P, P, P]),
     "asw_aggregate_den": (I, [PP, P, P, P, P, P, P, P, P, P]),
     "asw_wta": (I, [PP, P, P, P, P, P, P, P, P]),
     "asw_consistency": (I, [PP, P, P, P, P, P, P, P, P, P]),
     "asw_wta_local": (I, [PP, P, P, P, P, P]),
-    "asw_aggregate_pass_wta_local": (I, [PP, P, P, P, P, P, P, P, P, P]),
-    "asw_pass_wta_local_supported": (I, [PP]),
     "asw_wta_target_local": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_second": (I, [PP, P, P, P, P, P, P]),
     "asw_wta_finalize": (I, [PP, P, P, P, P, P, P, P, P, P, P, P]),

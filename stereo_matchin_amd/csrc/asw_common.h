@@ -34,41 +34,20 @@ void set_hip_error(hipError_t e);
 // last plane + 1 of the context's disparity shard (asw_params.d_end < 0: ndisp)
 __host__ __device__ inline int d_end_of_p(const asw_params *p) { return p->d_end < 0 ? p->ndisp : p->d_end; }
 
-// images of a V pass with the raw cost fused (asw_aggregate_pass_raw)
+// the first V pass over the raw costs as uint16 (asw_raw_cost16, asw_aggregate_pass_den16)
 struct RawSrc {
-    const uint8_t *left, *right;
-    const uint16_t *cost16;  // (left = right = NULL) the raw costs as uint16 (asw_raw_cost16)
-};
-
-// right support weights of an H pass computed on the fly (asw_aggregate_pass_otf):
-// the right RGBA8 image and the support LUT (asw_support_lut)
-struct OtfSrc {
-    const uint8_t *right;
-    const float *lut;
-};
-
-// the local WTA scan fused into the last H pass (asw_aggregate_pass_wta_local): per
-// pixel key = (m1 bits << 32 | first argmin d), INT64_MAX where no plane is below the
-// sentinel, m1 and m2 over the volume's planes: what k_wta_local_scan writes
-struct WtaLocalOut {
-    long long *key;
-    float *m1, *m2;
+    const uint16_t *cost16;
 };
 
 // one aggregation pass over every local plane (asw_aggregate.hip)
 // den/dm: cached-denominator mode (ASW_DEN_*; den = NULL with ASW_DEN_NONE)
 int launch_pass(const asw_params *p, int dir, const float *wl, const float *wr, const float *cin, float *cout,
-                float *den, int dm, hipStream_t st, const RawSrc *raw = nullptr, const OtfSrc *otf = nullptr);
-// an H den-read pass with the local WTA scan fused (asw_aggregate_pass_wta_local)
-int launch_pass_wta_local(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
-                          const float *den, const WtaLocalOut &o, hipStream_t st);
-bool pass_wta_local_supported(const asw_params *p);
+                float *den, int dm, hipStream_t st, const RawSrc *raw = nullptr);
 // the H pass's k_hpass11 segment length (variant bits 8..11: U-step chunks, else the
 // multiple of U nearest 240) and its choice against k_hpass9 (launch_dm)
 int h11_seg_len(int T, int variant);
 bool h11_selected(const asw_params *p, int variant);
-// the tap counts with ring kernels (the ones asw_aggregate_pass_otf and the fused
-// raw-cost pass support)
+// the tap counts with ring kernels (the uint16 first pass needs one)
 bool ring_taps(int T);
 int set_pass_variant(int v);
 // the asw_tune_set(ASW_TUNE_PASS_VARIANT) bits launch_dm reads: 128 = H by k_hpass9,

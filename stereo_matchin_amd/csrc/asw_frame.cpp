@@ -39,14 +39,8 @@ struct Shard {
     float *wvl = nullptr, *wvr = nullptr, *whl = nullptr, *whr = nullptr;  // [H][W][Tp]
     float *c0 = nullptr, *c1 = nullptr;                                    // [H][W][Dp]
     float *den_v = nullptr, *den_h = nullptr;  // cached denominators (iters >= 2)
-    bool otf = false;  // the H passes compute the right weights on the fly (whr not allocated)
-    bool vidx = false; // wvl / wvr in index form (uint16 LUT indices; asw_aggregate_pass_index)
-    bool hidx = false; // whl / whr likewise
-    bool fuse = false; // asw_Aggr fused into the first V pass (asw_aggregate_pass_raw)
     bool raw16 = false; // the raw costs as uint16 in c0 (asw_raw_cost16 + asw_aggregate_pass_den16)
-    bool otfv = false;  // a 32-plane shard's V passes compute both weights (wvl / wvr not allocated)
-    bool wtaf = false;  // the last H pass runs the WTA's local scan (asw_aggregate_pass_wta_local) into key / m1 / m2
-    // d-sharded WTA (more than one shard in the frame, or the fused local scan)
+    // d-sharded WTA (more than one shard in the frame)
     int64_t *key = nullptr, *key_g = nullptr, *tkey = nullptr, *tkey_g = nullptr;
     float *m1 = nullptr, *m2 = nullptr, *t1 = nullptr, *t2 = nullptr, *m2_g = nullptr, *t2_g = nullptr;
     ncclComm_t comm = nullptr;
@@ -263,58 +257,24 @@ int alloc_shard(Shard &s, bool sharded) {
         ASWCHK(dev_alloc(&s.lab_l, asw_lab_bytes(p)));
         ASWCHK(dev_alloc(&s.lab_r, asw_lab_bytes(p)));
     }
-    // asw_Aggr fused into the first V pass (k_vpass10_raw): the raw-cost volume is never
-    // written nor read, bit-identical, but measured slower at C4 (2.40 ms against 0.37 +
-    // 1.78 ms; frame 23.40 either way, profiles/r04/fused_raw_r10d.log), so the two
-    // kernels stay the default; ASW_FLAG_FUSE_RAW selects the fused pass
-    s.fuse = (p->flags & ASW_FLAG_FUSE_RAW) && asw_pass_raw_supported(p);
-    // a 32-plane shard can read its supports in index form (uint16 LUT
-    // indices, half the bytes of the replicated support stream; asw_aggregate_pass_index),
-    // bit-identical but measured slower: its passes are LDS-bound and the LUT reads cost
-    // more LDS cycles than the bytes save (C4 / 8: V 0.351 against 0.265 ms, H 0.68 against
-    // 0.36; shard frame 7.10 against 5.13 ms, profiles/r04/index_form_r10b.log).  Opt-in:
-    // ASW_FLAG_SUPPORT_INDEX (both directions) or ASW_FLAG_SUPPORT_INDEX_V (the V passes only)
-    const bool idx_on = p->flags & (ASW_FLAG_SUPPORT_INDEX | ASW_FLAG_SUPPORT_INDEX_V);
-    const bool v_only = !(p->flags & ASW_FLAG_SUPPORT_INDEX);
-    // ASW_FLAG_OTF_V, a 32-plane shard's V passes compute both weights from
-    // the images and the LUT (asw_aggregate_pass_otf_v; the V arrays are never built)
-    s.otfv = (p->flags & ASW_FLAG_OTF_V) && asw_pass_otf_v_supported(p) != 0;
-    s.vidx = !s.otfv && idx_on && asw_pass_index_supported(p, ASW_DIR_V, ASW_DEN_NONE) != 0;
-    s.hidx = idx_on && !v_only && s.vidx && asw_pass_index_supported(p, ASW_DIR_H, ASW_DEN_READ) != 0;
     // the raw-cost volume as uint16 (half the bytes written by asw_Aggr and read by the
-    // first V pass; bit-identical), where built and not replaced by the fused or
-    // index-form first pass; ASW_FLAG_RAW_F32 keeps the float volume
-    s.raw16 = !s.fuse && !s.vidx && !s.otfv && !(p->flags & ASW_FLAG_RAW_F32) && asw_raw16_supported(p);
-    const size_t vbytes = s.vidx ? asw_support_index_bytes(p) : asw_support_bytes(p);
-    const size_t hbytes = s.hidx ? asw_support_index_bytes(p) : asw_support_bytes(p);
-    if (!s.otfv) {
-        ASWCHK(dev_alloc(&s.wvl, vbytes));
-        ASWCHK(dev_alloc(&s.wvr, vbytes));
-    }
-    ASWCHK(dev_alloc(&s.whl, hbytes));
-    // the right H weights can be computed inside the H passes
-    // (asw_aggregate_pass_otf, the array then never built): bit-identical but measured
-    // slower at C4 (H den-read 2.30 against 1.42 ms), so only on request (ASW_FLAG_OTF_H)
-    s.otf = (p->flags & ASW_FLAG_OTF_H) && asw_pass_otf_supported(p, ASW_DIR_H) != 0;
-    if (!s.otf) ASWCHK(dev_alloc(&s.whr, hbytes));
+    // first V pass; bit-identical) where built; ASW_FLAG_RAW_F32 keeps the float volume
+    s.raw16 = !(p->flags & ASW_FLAG_RAW_F32) && asw_raw16_supported(p);
+    ASWCHK(dev_alloc(&s.wvl, asw_support_bytes(p)));
+    ASWCHK(dev_alloc(&s.wvr, asw_support_bytes(p)));
+    ASWCHK(dev_alloc(&s.whl, asw_support_bytes(p)));
+    ASWCHK(dev_alloc(&s.whr, asw_support_bytes(p)));
     ASWCHK(dev_alloc(&s.c0, asw_cost_bytes(p)));
     ASWCHK(dev_alloc(&s.c1, asw_cost_bytes(p)));
-    if (p->iters >= 2) {  // the den of a direction is written by its first pass and read by the r-1 others
+    if (p->iters >= 2 && asw_disp_pitch(p) != 32) {
+        // the den of a direction is written by its first pass and read by the r-1 others
         // (a 32-plane shard's passes recompute it: at C4 / 8 k_vpass32 den-none 0.24 against
         // den-read 0.28 ms, k_hpass32 0.30-0.33 against 0.36, profiles/r04/h32_variants_r11d.log;
-        // ASW_FLAG_SHARD_DEN_H keeps the H pass reading it)
-        const bool p32 = asw_disp_pitch(p) == 32;
-        if (!p32) ASWCHK(dev_alloc(&s.den_v, asw_cost_bytes(p)));
-        if (!p32 || (p->flags & ASW_FLAG_SHARD_DEN_H)) ASWCHK(dev_alloc(&s.den_h, asw_cost_bytes(p)));
+        // in the shard frame 4.99 against 5.04 ms, profiles/r04/shard_den_h_ab_r11e.log)
+        ASWCHK(dev_alloc(&s.den_v, asw_cost_bytes(p)));
+        ASWCHK(dev_alloc(&s.den_h, asw_cost_bytes(p)));
     }
-    // ASW_FLAG_WTA_FUSED: the WTA's own scan inside the last H pass where that pass is one
-    // k_hpass11 block over every plane (asw_pass_wta_local_supported); bit-identical maps,
-    // measured slower at C4 (the pass 1.87 against 1.45 ms at 3 instead of 4 blocks per
-    // CU, and the separate target scan 0.29 against asw_wta's 0.57 in all: 23.02-23.06
-    // against 22.95 ms)
-    s.wtaf = (p->flags & ASW_FLAG_WTA_FUSED) && !s.otf && !s.hidx && s.den_h && p->iters >= 2 &&
-             asw_pass_wta_local_supported(p) != 0;
-    if (sharded || s.wtaf) {
+    if (sharded) {
         ASWCHK(dev_alloc(&s.key, S * 8));
         ASWCHK(dev_alloc(&s.key_g, S * 8));
         ASWCHK(dev_alloc(&s.tkey, S * 8));
@@ -457,9 +417,9 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         HIPCHK(hipMemcpyAsync(s.right, right_rgba, S * 4, hipMemcpyHostToDevice, st));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_raw], st));
-    // the raw cost: its own kernel, or (s.fuse) computed inside the first V pass
+    // the raw cost (uint16 where the first pass reads it so)
     if (s.raw16) ASWCHK(asw_raw_cost16(p, s.left, s.right, reinterpret_cast<uint16_t *>(s.c0), st));
-    else if (!s.fuse) ASWCHK(asw_raw_cost(p, s.left, s.right, s.c0, st));
+    else ASWCHK(asw_raw_cost(p, s.left, s.right, s.c0, st));
     if (timed) HIPCHK(hipEventRecord(c->ev[e_raw + 1], st));
     if (p->color_space == ASW_COLOR_LAB) {
         ASWCHK(asw_lab(p, s.left, s.lab_l, st));
@@ -470,51 +430,27 @@ int shard_aggregate(asw_ctx *c, int i, const uint8_t *left_rgba, const uint8_t *
         ASWCHK(asw_support_lab(p, ASW_DIR_H, s.lab_r, s.whr, st));
     } else {
         ASWCHK(asw_support_lut(p, s.lut, st));
-        ASWCHK(asw_support_all_fmt(p, s.left, s.right, s.lut, s.otfv ? nullptr : s.wvl, s.whl,
-                                   s.otfv ? nullptr : s.wvr, s.otf ? nullptr : s.whr,
-                                   (s.vidx ? 5 : 0) | (s.hidx ? 10 : 0), st));
+        ASWCHK(asw_support_all(p, s.left, s.right, s.lut, s.wvl, s.whl, s.wvr, s.whr, st));
     }
     if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0], st));
     for (int it = 0; it < p->iters; ++it) {
         const int dmv = !s.den_v ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
         const int dm = !s.den_h ? ASW_DEN_NONE : (it == 0 ? ASW_DEN_WRITE : ASW_DEN_READ);
-        if (it == 0 && s.fuse)
-            ASWCHK(asw_aggregate_pass_raw(p, s.wvl, s.wvr, s.left, s.right, s.c1, s.den_v, dmv, st));
-        else if (s.otfv)
-            ASWCHK(asw_aggregate_pass_otf_v(p, s.left, s.right, s.lut, s.c0, s.c1, st));
-        else if (it == 0 && s.raw16)
+        if (it == 0 && s.raw16)
             ASWCHK(asw_aggregate_pass_den16(p, s.wvl, s.wvr, reinterpret_cast<const uint16_t *>(s.c0), s.c1, s.den_v,
                                             dmv, st));
-        else if (s.vidx)
-            ASWCHK(asw_aggregate_pass_index(p, ASW_DIR_V, reinterpret_cast<const uint16_t *>(s.wvl),
-                                            reinterpret_cast<const uint16_t *>(s.wvr), s.lut, s.c0, s.c1, nullptr,
-                                            ASW_DEN_NONE, st));
         else ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_V, s.wvl, s.wvr, s.c0, s.c1, s.den_v, dmv, st));
         if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0 + 2 * it + 1], st));
-        if (s.otf) ASWCHK(asw_aggregate_pass_otf(p, ASW_DIR_H, s.whl, s.right, s.lut, s.c1, s.c0, s.den_h, dm, st));
-        else if (s.hidx)
-            ASWCHK(asw_aggregate_pass_index(p, ASW_DIR_H, reinterpret_cast<const uint16_t *>(s.whl),
-                                            reinterpret_cast<const uint16_t *>(s.whr), s.lut, s.c1, s.c0, s.den_h, dm,
-                                            st));
-        else if (s.wtaf && it == p->iters - 1)
-            ASWCHK(asw_aggregate_pass_wta_local(p, s.whl, s.whr, s.c1, s.c0, s.den_h, s.key, s.m1, s.m2, st));
-        else ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, s.whl, s.whr, s.c1, s.c0, s.den_h, dm, st));
+        ASWCHK(asw_aggregate_pass_den(p, ASW_DIR_H, s.whl, s.whr, s.c1, s.c0, s.den_h, dm, st));
         if (timed) HIPCHK(hipEventRecord(c->ev[e_pass0 + 2 * it + 2], st));
     }
     return ASW_OK;
 }
 
-// The WTA of a one-shard frame: asw_wta, or, when the last pass ran the local scan,
-// the rest of the one-shard protocol (the target scan and the finalize; a single shard's
-// second minima are its own)
+// The WTA of a one-shard frame
 int single_wta(asw_ctx *c) {
     Shard &s0 = c->sh[0];
-    if (!s0.wtaf)
-        return asw_wta(&s0.p, s0.c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar,
-                       s0.stream);
-    ASWCHK(asw_wta_target_local(&s0.p, s0.c0, s0.key, s0.tkey, s0.t1, s0.t2, s0.stream));
-    return asw_wta_finalize(&s0.p, s0.key, s0.m2, s0.tkey, s0.t2, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar,
-                            c->code_ref, c->code_tar, s0.stream);
+    return asw_wta(&s0.p, s0.c0, c->d_ref, c->conf_ref, c->d_tar, c->conf_tar, c->code_ref, c->code_tar, s0.stream);
 }
 
 // The d-sharded WTA (asw_wta_local protocol, include/asw.h): maps on shard 0.
@@ -523,7 +459,7 @@ int sharded_wta(asw_ctx *c) {
     for (int i = 0; i < c->n; ++i) {
         Shard &s = c->sh[i];
         HIPCHK(hipSetDevice(s.device));
-        if (!s.wtaf) ASWCHK(asw_wta_local(&s.p, s.c0, s.key, s.m1, s.m2, s.stream));  // (else: the last pass's)
+        ASWCHK(asw_wta_local(&s.p, s.c0, s.key, s.m1, s.m2, s.stream));
         HIPCHK(hipMemcpyAsync(s.key_g, s.key, S * 8, hipMemcpyDeviceToDevice, s.stream));
     }
     ASWCHK(allreduce_min<int64_t>(c, b_key_g, ncclInt64));

@@ -170,9 +170,8 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
 // ---------------------------------------------------------------------------
 struct SupportJobs {
     const uchar4 *img[4];
-    float *w[4];  // (index form: uint16_t [H][W][Tp] behind the pointer)
+    float *w[4];
     int dir[4];
-    int idx[4];   // 1: write the LUT index dist*766 + SAD of each weight (asw_support_all_fmt)
 };
 // (Round 4's EXPD form, each weight's exp computed instead of gathered, measured
 // slower and moved to tools/exp/exp_forms.hip.)
@@ -223,41 +222,6 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
         for (int k = 0; k < 4 * NG; ++k) b[k] = win[wbase + k * wstep];
         __syncthreads();  // every wave holds its neighbours: the tile is the staging tile again
         if (!live) return;
-        if (jobs.idx[blockIdx.z]) {
-            // index form: the weight's LUT index instead of the weight (no gathers),
-            // four uint16 per 8-B share, transposed through LDS like the weights
-            using u2 = unsigned __attribute__((ext_vector_type(2)));
-            u2 c[NG];
-#pragma unroll
-            for (int k = 0; k < 4 * NG; ++k) {
-                int dist;
-                if (dir == ASW_DIR_V) {
-                    const int qy = clampi(y + k - R, 0, H - 1);
-                    dist = y > qy ? y - qy : qy - y;
-                } else {
-                    const int qx = clampi(x + k - R, 0, W - 1);
-                    dist = x > qx ? x - qx : qx - x;
-                }
-                const int sad = (int)__builtin_amdgcn_sad_u8(a, b[k], 0u);
-                const unsigned ix = k < T ? (unsigned)(dist * kLutWidth + sad) : 0u;
-                if (k % 2 == 0) c[k / 4][(k % 4) / 2] = ix;
-                else c[k / 4][(k % 4) / 2] |= ix << 16;
-            }
-            u2 *st2 = reinterpret_cast<u2 *>(stg[wv]);
-#pragma unroll
-            for (int g = 0; g < NG; ++g) st2[lane * Q + g] = c[g];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int nval = min(64, W - x0) * Q;
-            u2 *out = reinterpret_cast<u2 *>(jobs.w[blockIdx.z]) + ((long long)y * W + x0) * Q;
-#pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                const int e = g * 64 + lane;
-                if (e < nval) out[e] = st2[e];
-            }
-            return;
-        }
         f4 v[NG];
 #pragma unroll
         for (int k = 0; k < 4 * NG; ++k) {
@@ -405,9 +369,6 @@ __global__ __launch_bounds__(256) void k_support_lab(const float4 *__restrict__ 
 // ---------------------------------------------------------------------------
 constexpr float kInit = 100000.0f;  // K/asw_wta.cl:25-26
 
-__device__ __forceinline__ long long make_key(float v, int idx) {
-    return (long long)(((unsigned long long)__float_as_uint(v) << 32) | (unsigned)idx);
-}
 constexpr long long kNoKey = 0x7fffffffffffffffLL;
 
 // second-smallest contribution: the shard that owns the global minimum offers
@@ -524,14 +485,6 @@ using namespace asw;
 // C-ABI: parameters and layout
 // ===========================================================================
 namespace asw {
-// asw_aggregate.hip: the pass over index-form supports
-bool pass_index_supported(const asw_params *p, int dir, int dm);
-int launch_pass_index(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
-                      const float *cin, float *cout, float *den, int dm, hipStream_t st);
-// asw_aggregate.hip: the shard V pass with both weights on the fly
-bool pass_otf_v_supported(const asw_params *p);
-int launch_pass_otf_v(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut,
-                      const float *cin, float *cout, hipStream_t st);
 // asw_wta_sweep.hip: asw_WTA as a row sweep (ASW_E_UNSUPPORTED for pitches it is not built for)
 int launch_wta_sweep(const asw_params *p, const float *cost, int32_t *d_ref, float *conf_ref, int32_t *d_tar,
                      float *conf_tar, uint8_t *code_ref, uint8_t *code_tar, hipStream_t st);
@@ -542,6 +495,7 @@ extern "C" {
 // 2: asw_outputs gained disp16 / lr16 and asw_timings gained exchange (round 2);
 // asw_create rejects shapes the pass kernels cannot address (ASW_E_UNSUPPORTED)
 // 3: asw_params.flags (round 5)
+// 4: the measured-negative forms and their flags removed (round 6)
 int asw_abi_version(void) { return ASW_ABI_VERSION; }
 
 // 0: lane-per-pixel scans (default), 2: asw_WTA by the row sweep (asw_wta_sweep.hip;
@@ -553,10 +507,9 @@ int asw_tune_set(int key, int value) {
     if (key == ASW_TUNE_PASS_VARIANT) {
         // only bits that select a compiled form (launch_dm): a stale bit would time the
         // default kernel under another name
-        // (+ bits 16-27: strip / segment counts, the H form, the index-form H phases, the
-        // nt policy flip and the lean H form's left ring in LDS (the default: DPP rows) of
-        // the 32-plane shard passes, asw_pass32.h)
-        if (value & ~(asw::kPassVariantBits | 0xFFF0000)) return ASW_E_INVALID;
+        // (+ bits 16-23: strip / segment counts, and bit 26: the nt policy flip of the
+        // 32-plane shard passes, asw_pass32.h)
+        if (value & ~(asw::kPassVariantBits | 0xFF0000 | (1 << 26))) return ASW_E_INVALID;
         return asw::set_pass_variant(value);
     }
     if (key == ASW_TUNE_WTA_VARIANT) {
@@ -691,10 +644,6 @@ int asw_support_lut(const asw_params *p, float *lut, void *stream) {
 
 static int launch_support(const asw_params *p, const SupportJobs &jobs, int njobs, const float *lut, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
-    bool any_idx = false;
-    for (int j = 0; j < njobs; ++j) any_idx = any_idx || jobs.idx[j];
-    // index form: uint16 indices of the (R+1) x 766 LUT, the unrolled kernels only
-    if (any_idx && ((p->taps / 2 + 1) * kLutWidth > 65536 || asw_tap_pitch(p) > 68)) return ASW_E_UNSUPPORTED;
     switch (asw_tap_pitch(p) / 4) {  // Tp = 4Q, Q odd past 1 (tap_pitch)
         case 1: launch_support_q<1>(p, jobs, njobs, lut, st); break;
         case 3: launch_support_q<3>(p, jobs, njobs, lut, st); break;
@@ -725,34 +674,21 @@ int asw_support(const asw_params *p, int dir, const uint8_t *img, const float *l
     return launch_support(p, jobs, 1, lut, stream);
 }
 
-int asw_support_all_fmt(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut, void *wvl,
-                        void *whl, void *wvr, void *whr, int index_mask, void *stream) {
+int asw_support_all(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut, float *wvl,
+                    float *whl, float *wvr, float *whr, void *stream) {
     ASW_CHECK_PARAMS(p);
-    if (!left || !right || !lut || !(wvl || whl || wvr || whr) || (index_mask & ~15)) return ASW_E_INVALID;
+    if (!left || !right || !lut || !wvl || !whl || !wvr || !whr) return ASW_E_INVALID;
     if (p->color_space != ASW_COLOR_RGB) return ASW_E_INVALID;
     SupportJobs jobs{};
     const uchar4 *img[4] = {reinterpret_cast<const uchar4 *>(left), reinterpret_cast<const uchar4 *>(left),
                             reinterpret_cast<const uchar4 *>(right), reinterpret_cast<const uchar4 *>(right)};
-    void *w[4] = {wvl, whl, wvr, whr};
-    int n = 0;
+    float *w[4] = {wvl, whl, wvr, whr};
     for (int j = 0; j < 4; ++j) {
-        if (!w[j]) continue;  // an array the caller computes on the fly (asw_aggregate_pass_otf)
-        jobs.img[n] = img[j];
-        jobs.w[n] = static_cast<float *>(w[j]);
-        jobs.dir[n] = (j & 1) ? ASW_DIR_H : ASW_DIR_V;
-        jobs.idx[n] = (index_mask >> j) & 1;
-        ++n;
+        jobs.img[j] = img[j];
+        jobs.w[j] = w[j];
+        jobs.dir[j] = (j & 1) ? ASW_DIR_H : ASW_DIR_V;
     }
-    return launch_support(p, jobs, n, lut, stream);
-}
-
-int asw_support_all(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut, float *wvl,
-                    float *whl, float *wvr, float *whr, void *stream) {
-    return asw_support_all_fmt(p, left, right, lut, wvl, whl, wvr, whr, 0, stream);
-}
-
-size_t asw_support_index_bytes(const asw_params *p) {
-    return (size_t)p->width * p->height * (size_t)asw_tap_pitch(p) * sizeof(uint16_t);
+    return launch_support(p, jobs, 4, lut, stream);
 }
 
 int asw_lab(const asw_params *p, const uint8_t *img, float *lab, void *stream) {
@@ -793,71 +729,6 @@ int asw_aggregate_pass_den(const asw_params *p, int dir, const float *wl, const 
     return asw::launch_pass(p, dir, wl, wr, cin, cout, den, den_mode, (hipStream_t)stream);
 }
 
-int asw_aggregate_pass_otf(const asw_params *p, int dir, const float *wl, const uint8_t *right_rgba, const float *lut,
-                           const float *cin, float *cout, float *den, int den_mode, void *stream) {
-    ASW_CHECK_PARAMS(p);
-    if (!wl || !right_rgba || !lut || !cin || !cout || cin == cout) return ASW_E_INVALID;
-    if (den_mode < ASW_DEN_NONE || den_mode > ASW_DEN_READ) return ASW_E_INVALID;
-    if (den_mode != ASW_DEN_NONE && (!den || den == cin || den == cout)) return ASW_E_INVALID;
-    if (dir != ASW_DIR_H || p->color_space != ASW_COLOR_RGB || !asw::ring_taps(p->taps)) return ASW_E_UNSUPPORTED;
-    const asw::OtfSrc otf{right_rgba, lut};
-    return asw::launch_pass(p, dir, wl, nullptr, cin, cout, den, den_mode, (hipStream_t)stream, nullptr, &otf);
-}
-
-int asw_aggregate_pass_index(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
-                             const float *cin, float *cout, float *den, int den_mode, void *stream) {
-    ASW_CHECK_PARAMS(p);
-    if (!wl || !wr || !lut || !cin || !cout || cin == cout || (dir != ASW_DIR_V && dir != ASW_DIR_H))
-        return ASW_E_INVALID;
-    if (den_mode < ASW_DEN_NONE || den_mode > ASW_DEN_READ) return ASW_E_INVALID;
-    if (den_mode != ASW_DEN_NONE && (!den || den == cin || den == cout)) return ASW_E_INVALID;
-    return asw::launch_pass_index(p, dir, wl, wr, lut, cin, cout, den, den_mode, (hipStream_t)stream);
-}
-
-int asw_pass_otf_v_supported(const asw_params *p) {
-    if (!p || asw_params_check(p) != ASW_OK) return 0;
-    return asw::pass_otf_v_supported(p) ? 1 : 0;
-}
-
-int asw_aggregate_pass_otf_v(const asw_params *p, const uint8_t *left_rgba, const uint8_t *right_rgba,
-                             const float *lut, const float *cin, float *cout, void *stream) {
-    ASW_CHECK_PARAMS(p);
-    if (!left_rgba || !right_rgba || !lut || !cin || !cout || cin == cout) return ASW_E_INVALID;
-    return asw::launch_pass_otf_v(p, left_rgba, right_rgba, lut, cin, cout, (hipStream_t)stream);
-}
-
-int asw_pass_wta_local_supported(const asw_params *p) {
-    if (!p || asw_params_check(p) != ASW_OK) return 0;
-    return asw::pass_wta_local_supported(p) ? 1 : 0;
-}
-
-int asw_aggregate_pass_wta_local(const asw_params *p, const float *supp_left, const float *supp_right,
-                                 const float *cin, float *cout, const float *den, int64_t *key, float *m1, float *m2,
-                                 void *stream) {
-    ASW_CHECK_PARAMS(p);
-    if (!supp_left || !supp_right || !cin || !cout || !den || !key || !m1 || !m2 || cin == cout) return ASW_E_INVALID;
-    const asw::WtaLocalOut o{reinterpret_cast<long long *>(key), m1, m2};
-    return asw::launch_pass_wta_local(p, supp_left, supp_right, cin, cout, den, o, (hipStream_t)stream);
-}
-
-int asw_pass_index_supported(const asw_params *p, int dir, int den_mode) {
-    if (!p || asw_params_check(p) != ASW_OK) return 0;
-    return asw::pass_index_supported(p, dir, den_mode) ? 1 : 0;
-}
-
-int asw_pass_otf_supported(const asw_params *p, int dir) {
-    if (!p || asw_params_check(p) != ASW_OK) return 0;
-    // (a 32-plane shard's half-wave H pass reads the materialised array)
-    return dir == ASW_DIR_H && p->color_space == ASW_COLOR_RGB && asw::ring_taps(p->taps) && asw_disp_pitch(p) != 32
-               ? 1 : 0;
-}
-
-int asw_pass_raw_supported(const asw_params *p) {
-    if (!p || asw_params_check(p) != ASW_OK) return 0;
-    // ring kernels only (in a make DEV=1 library: its one tap count), not a 32-plane shard
-    return p->iters >= 1 && asw::ring_taps(p->taps) && asw_disp_pitch(p) != 32 ? 1 : 0;
-}
-
 int asw_aggregate_pass_den16(const asw_params *p, const float *wvl, const float *wvr, const uint16_t *cin16,
                              float *cout, float *den, int den_mode, void *stream) {
     ASW_CHECK_PARAMS(p);
@@ -865,17 +736,7 @@ int asw_aggregate_pass_den16(const asw_params *p, const float *wvl, const float 
     if (den_mode != ASW_DEN_NONE && den_mode != ASW_DEN_WRITE) return ASW_E_INVALID;  // a first pass
     if (den_mode != ASW_DEN_NONE && (!den || den == cout)) return ASW_E_INVALID;
     if (!asw_raw16_supported(p)) return ASW_E_UNSUPPORTED;
-    const asw::RawSrc raw{nullptr, nullptr, cin16};
-    return asw::launch_pass(p, ASW_DIR_V, wvl, wvr, nullptr, cout, den, den_mode, (hipStream_t)stream, &raw);
-}
-
-int asw_aggregate_pass_raw(const asw_params *p, const float *wvl, const float *wvr, const uint8_t *left_rgba,
-                           const uint8_t *right_rgba, float *cout, float *den, int den_mode, void *stream) {
-    ASW_CHECK_PARAMS(p);
-    if (!wvl || !wvr || !left_rgba || !right_rgba || !cout) return ASW_E_INVALID;
-    if (den_mode < ASW_DEN_NONE || den_mode > ASW_DEN_READ) return ASW_E_INVALID;
-    if (den_mode != ASW_DEN_NONE && (!den || den == cout)) return ASW_E_INVALID;
-    const asw::RawSrc raw{left_rgba, right_rgba};
+    const asw::RawSrc raw{cin16};
     return asw::launch_pass(p, ASW_DIR_V, wvl, wvr, nullptr, cout, den, den_mode, (hipStream_t)stream, &raw);
 }
 

@@ -33,7 +33,6 @@ namespace asw {
 namespace agg {
 
 constexpr int kPlanes32 = 32;
-using u2 = unsigned __attribute__((ext_vector_type(2)));  // four uint16 LUT indices
 
 // taps [B, E) of a phase with per-lane left weights (wl, wr hold taps from B)
 template <int U, int S, int B, int E, bool DEN, int M>
@@ -73,28 +72,11 @@ __device__ __forceinline__ void taps32_dl(float &num, float &den, const f4 &wl, 
 // NBUF-deep LDS ring of row slabs written LEAD rows ahead, one barrier per RB rows,
 // weights in NPH phases with two phases' sets live).
 // ---------------------------------------------------------------------------
-//
-// IDX: the support arrays are in index form (asw_support_all_fmt: uint16 LUT indices,
-// half the bytes): the block copies the LUT into LDS once and each staged float4 is
-// looked up there (4 ds_read_b32) before it enters the slab ring; the taps then run
-// on the same float weights, so the result is bit-identical.
 // C16: the first V pass over the uint16 raw costs (asw_raw_cost16), as k_vpass10<C16>.
-// OTF: both support weights of a slab row computed in the pass from the
-// two images and the LUT (wl / wr are the left / right RGBA8 images, lut the global
-// asw_support_lut table), so the V support arrays are never built nor read.  The
-// staging shares are assigned tap-group-major (a wave's lanes = consecutive entries of
-// one float4 group q): each pixel load is one row's consecutive pixels and the LUT
-// gathers of a wave fall in one 3-KB LUT row (dist = |4q + j - R| but at the image
-// edges).  Each weight is k_support's: lut[|y - qy|][SAD(img(y, c), img(qy, c))],
-// qy = clamp(y + i - R), 0 for taps i >= T, so the slab holds the same floats.
-// Pipeline: the pixels of a row are loaded PSO steps before its gathers, which are
-// issued one step before the row is written to the slab.
-template <int T, int NW, int DM, int CP, int NPH, bool IDX = false, int RB = 2, int PS = 4, bool C16 = false,
-          bool OTF = false>
+template <int T, int NW, int DM, int CP, int NPH, int RB = 2, int PS = 4, bool C16 = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 4 : 2))) void k_vpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
-    float *__restrict__ den, int W, int H, int d_begin, int rows_per_strip, int nxb, int nstrip, int xg_per_xcd,
-    const float *__restrict__ lut) {
+    float *__restrict__ den, int W, int H, int d_begin, int rows_per_strip, int nxb, int nstrip, int xg_per_xcd) {
     constexpr int R = T / 2;
     constexpr int TP = tap_pitch(T);
     constexpr int Q = TP / 4;
@@ -104,10 +86,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     constexpr int LEAD = RB + 1;
     constexpr int NBUF = ring_div(U, 2 * RB + 1);
     static_assert(U % PS == 0 && U % KD == 0 && U % RB == 0 && U % NBUF == 0, "ring periods");
-    static_assert(OTF || LEAD <= PS, "staging ring too short for the barrier period");
-    static_assert(!OTF || (!IDX && !C16 && TP == 4 * Q), "on-the-fly weights: float supports, float input");
-    constexpr int PSO = 2;  // OTF: rows of pixels in flight
-    static_assert(!OTF || U % PSO == 0, "pixel ring period");
+    static_assert(LEAD <= PS, "staging ring too short for the barrier period");
     constexpr int LA = cmax(cmax(R + P, LEAD + PS), KD);  // rows past y a step touches
     constexpr int NC = 2 * NW;                             // columns per block
     constexpr int NER = NC + 31;                           // right entries per row
@@ -116,8 +95,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     constexpr int NSTAGE = (NQ + NW * 64 - 1) / (NW * 64);
     static_assert(NSTAGE <= 2, "slab row larger than two float4 per thread");
     __shared__ f4 slab[NBUF][NQ];
-    constexpr int NLUT = IDX ? (R + 1) * kLutWidth : 1;
-    __shared__ float lut_s[NLUT];
 
     const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
     const int xg = xcd * xg_per_xcd + m % xg_per_xcd;
@@ -171,72 +148,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     };
     const int o0 = src_of(t0), o1 = src_of(t1);
     const bool r0 = t0 / Q < NER, r1 = t1 / Q < NER;
-    // OTF: thread t computes share (q = t / NE, entry e = t % NE), stored at slab index
-    // e * Q + q (the layout above); its pixel column and image, and its taps 4q .. 4q+3
-    const int ot = min((int)threadIdx.x, NQ - 1);
-    const int oq = ot / NE, oe = ot - oq * NE;
-    const int oslot = oe * Q + oq;
-    const int ocol = oe < NER ? clampi(x0 - d_begin - 31 + oe, 0, W - 1) : min(x0 + oe - NER, W - 1);
-    const unsigned *__restrict__ oimg = reinterpret_cast<const unsigned *>(oe < NER ? wr : wl);
-    struct Px {
-        unsigned c, n[4];  // RGBA8 of the entry pixel at row y and of its taps' rows
-    };
-    auto px_load = [&](int row) __attribute__((always_inline)) {
-        Px v;
-        v.c = oimg[(long long)row * W + ocol];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v.n[j] = oimg[(long long)clampi(row + 4 * oq + j - R, 0, H - 1) * W + ocol];
-        return v;
-    };
-    auto px_gather = [&](const Px &v, int row) __attribute__((always_inline)) {
-        f4 w;
-        const unsigned c = v.c & 0xFFFFFFu;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = 4 * oq + j;
-            const int qy = clampi(row + i - R, 0, H - 1);
-            const int dist = row > qy ? row - qy : qy - row;
-            const unsigned sad = __builtin_amdgcn_sad_u8(c, v.n[j] & 0xFFFFFFu, 0u);  // |dR|+|dG|+|dB|
-            w[j] = i < T ? lut[dist * kLutWidth + (int)sad] : 0.0f;
-        }
-        return w;
-    };
-    // staged share: 4 weights (f4) or 4 LUT indices (u2, two uint16 per dword)
-    using stg_t = std::conditional_t<IDX, u2, f4>;
-    using elem_t = std::conditional_t<IDX, uint16_t, float>;
-    const elem_t *src0 = reinterpret_cast<const elem_t *>(r0 ? wr : wl) + o0;
-    const elem_t *src1 = reinterpret_cast<const elem_t *>(r1 ? wr : wl) + o1;
-    auto stage = [&](stg_t &a, stg_t &b, int row) __attribute__((always_inline)) {
-        a = *reinterpret_cast<const stg_t *>(src0 + row * wrow);
-        if constexpr (NSTAGE > 1) b = *reinterpret_cast<const stg_t *>(src1 + row * wrow);
-    };
-    // the float4 of a staged share (IDX: four LUT reads from LDS)
-    auto weights = [&](const stg_t &a) __attribute__((always_inline)) {
-        if constexpr (IDX) {
-            f4 v;
-            v[0] = lut_s[a[0] & 0xFFFFu];
-            v[1] = lut_s[a[0] >> 16];
-            v[2] = lut_s[a[1] & 0xFFFFu];
-            v[3] = lut_s[a[1] >> 16];
-            return v;
-        } else {
-            return a;
-        }
+    const float *src0 = (r0 ? wr : wl) + o0;
+    const float *src1 = (r1 ? wr : wl) + o1;
+    auto stage = [&](f4 &a, f4 &b, int row) __attribute__((always_inline)) {
+        a = *reinterpret_cast<const f4 *>(src0 + row * wrow);
+        if constexpr (NSTAGE > 1) b = *reinterpret_cast<const f4 *>(src1 + row * wrow);
     };
     auto put = [&](int buf, const f4 &a, const f4 &b) __attribute__((always_inline)) {
         slab[buf][t0] = a;
         if constexpr (NSTAGE > 1) slab[buf][t1] = b;
     };
-    if constexpr (IDX) {
-        for (int t = threadIdx.x; t < NLUT; t += NW * 64) lut_s[t] = lut[t];
-        __syncthreads();
-    }
 
     using PH = Phases<T, NPH>;
     float win[U];
-    stg_t sa[OTF ? 1 : PS], sb[OTF ? 1 : PS];
-    Px px[OTF ? PSO : 1];
-    f4 gw;  // OTF: the gathered weights of the row written to the slab at the next step
+    f4 sa[PS], sb[PS];
     f4 wlp[NPH][PH::NG], wrp[NPH][PH::NG];
     float dring[KD];
     {
@@ -258,27 +183,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
 #pragma unroll
         for (int j = 0; j < KD; ++j) dring[j] = bload<CP>(rp, voff, (min(y_begin + j, H - 1) - y_begin) * rowbytes);
     }
-    if constexpr (OTF) {
-        // rows 0 .. LEAD-1 into the slab, row LEAD's gathers, rows LEAD+1 .. LEAD+PSO-1's pixels
 #pragma unroll
-        for (int j = 0; j < LEAD; ++j) {
-            const int row = min(y_begin + j, H - 1);
-            slab[j][oslot] = px_gather(px_load(row), row);
-        }
-        {
-            const int row = min(y_begin + LEAD, H - 1);
-            gw = px_gather(px_load(row), row);
-        }
+    for (int j = 0; j < PS; ++j) stage(sa[j], sb[j], min(y_begin + j, H - 1));
 #pragma unroll
-        for (int j = LEAD + 1; j < LEAD + PSO; ++j) px[j % PSO] = px_load(min(y_begin + j, H - 1));
-    } else {
+    for (int j = 0; j < LEAD; ++j) put(j, sa[j], sb[j]);
 #pragma unroll
-        for (int j = 0; j < PS; ++j) stage(sa[j], sb[j], min(y_begin + j, H - 1));
-#pragma unroll
-        for (int j = 0; j < LEAD; ++j) put(j, weights(sa[j]), weights(sb[j]));
-#pragma unroll
-        for (int j = 0; j < LEAD; ++j) stage(sa[j], sb[j], min(y_begin + PS + j, H - 1));
-    }
+    for (int j = 0; j < LEAD; ++j) stage(sa[j], sb[j], min(y_begin + PS + j, H - 1));
     __syncthreads();
     auto request = [&](auto kc, int buf) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
@@ -315,24 +225,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
                 else wait_lgkm0();
                 if constexpr (k == 0) asm volatile("" ::"v"(win[(s + T - 1) % U]));  // one vmcnt wait per step
                 __builtin_amdgcn_sched_barrier(0);
-                // (IDX: the staged row's LUT reads go out before the weight requests, so
-                // the slab write waits for them alone)
-                f4 pa, pb;
-                if constexpr (k == 0 && !OTF) {
-                    pa = weights(sa[(s + LEAD) % PS]);
-                    if constexpr (NSTAGE > 1) pb = weights(sb[(s + LEAD) % PS]);
-                }
                 if constexpr (k + 1 < NPH) request(std::integral_constant<int, k + 1>{}, bcur);
                 else request(std::integral_constant<int, 0>{}, bnext);
-                if constexpr (k == 0 && OTF) {
-                    // row y+LEAD (gathered a step ago) into the slab; row y+LEAD+1's gathers;
-                    // row y+LEAD+PSO's pixels into the slot row y+LEAD's pixels held
-                    slab[bput][oslot] = gw;
-                    const int rg = min(y + LEAD + 1, H - 1);
-                    gw = px_gather(px[(s + LEAD + 1) % PSO], rg);
-                    px[(s + LEAD) % PSO] = px_load(min(y + LEAD + PSO, H - 1));
-                } else if constexpr (k == 0) {
-                    put(bput, pa, pb);
+                if constexpr (k == 0) {
+                    put(bput, sa[(s + LEAD) % PS], sb[(s + LEAD) % PS]);
                     stage(sa[(s + LEAD) % PS], sb[(s + LEAD) % PS], min(y + LEAD + PS, H - 1));
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -378,18 +274,14 @@ constexpr int h32_batch(int T) { return tap_pitch(T) / 4 * 8 <= 64 * 4 ? 4 : 2; 
 
 // RING16: right ring of a multiple of 16 entries (conflict-free across the wrap) or
 // the minimal 32 + 2K (a 2-way conflict where a read wraps; less LDS, more waves)
-// IDX: index-form supports (uint16 LUT indices): the block's waves share one LDS copy
-// of the LUT, and each staged float4 is looked up there before it enters the ring.
 // KB: the refill batch (0: h32_batch).
 // (Round 5: the weights requested two phases ahead instead of one measured 0.3115
 // against 0.3173 ms per pass and the same shard frame, profiles/r05/pd2_nt_r12c.log;
 // not kept.)
-template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0,
-          bool DL = false>
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, int KB = 0, bool DL = false>
 __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_hpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
-    float *__restrict__ den, int W, int H, int d_begin, int nseg, int seg_len, int npairs, int pairs_per_xcd,
-    const float *__restrict__ lut) {
+    float *__restrict__ den, int W, int H, int d_begin, int nseg, int seg_len, int npairs, int pairs_per_xcd) {
     constexpr int R = T / 2;
     constexpr int TP = tap_pitch(T);
     constexpr int Q = TP / 4;
@@ -401,18 +293,12 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     constexpr int LRING = DL ? 0 : 2 * K + 2;          // left entries per row (not DL)
     constexpr int ROWE = RING + LRING;                 // ring entries per row
     static_assert(U % K == 0, "the batch top must be a compile-time step");
-    static_assert(!DL || (!IDX && (T + 3) / 4 <= 16), "DL: float supports, taps in one DPP row");
+    static_assert(!DL || (T + 3) / 4 <= 16, "DL: taps in one DPP row");
     // staged per batch: 2 rows x (K right + K left entries, DL: K right) x Q float4 over 64 lanes
     constexpr int NK = DL ? 1 : 2;
     constexpr int NST = 2 * NK * K * Q;
     constexpr int SPL = (NST + 63) / 64;  // float4 per lane
     __shared__ f4 ring_all[NWB][2 * ROWE * Q];
-    constexpr int NLUT = IDX ? (R + 1) * kLutWidth : 1;
-    __shared__ float lut_s[NLUT];
-    if constexpr (IDX) {  // (before any wave leaves: the one block barrier)
-        for (int t = threadIdx.x; t < NLUT; t += NWB * 64) lut_s[t] = lut[t];
-        __syncthreads();
-    }
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -435,23 +321,12 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     // n = ((r*2 + kind)*K + k)*Q + q: row r, kind 0 = right entry xb+1-d0+k, kind 1 =
     // left entry xb+1+k of the batch whose first step is xb (its entries are written at
     // the top of batch xb - K, the batch before the one that first reads them)
-    using stg_t = std::conditional_t<IDX, u2, f4>;  // a staged share: 4 weights or 4 LUT indices
-    using elem_t = std::conditional_t<IDX, uint16_t, float>;
-    const elem_t *wre = reinterpret_cast<const elem_t *>(wr), *wle = reinterpret_cast<const elem_t *>(wl);
+    using stg_t = f4;  // a staged share: 4 weights
+    using elem_t = float;
+    const elem_t *wre = wr, *wle = wl;
     const elem_t *wrrows[2] = {wre + (long long)min(2 * pr, H - 1) * W * TP, wre + (long long)min(2 * pr + 1, H - 1) * W * TP};
     const elem_t *wlrows[2] = {wle + (long long)min(2 * pr, H - 1) * W * TP, wle + (long long)min(2 * pr + 1, H - 1) * W * TP};
-    auto weights = [&](const stg_t &a) __attribute__((always_inline)) {
-        if constexpr (IDX) {
-            f4 v;
-            v[0] = lut_s[a[0] & 0xFFFFu];
-            v[1] = lut_s[a[0] >> 16];
-            v[2] = lut_s[a[1] & 0xFFFFu];
-            v[3] = lut_s[a[1] >> 16];
-            return v;
-        } else {
-            return a;
-        }
-    };
+    auto weights = [](const stg_t &a) __attribute__((always_inline)) { return a; };
     // (the share's row is a global-address-space pointer: a generic one compiles to
     // flat loads, which also count against lgkmcnt, so every LDS wait of the step loop
     // would wait for the staging loads of the next batch as well; the clamp is the
@@ -493,7 +368,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
         } else {
             const int x = xs + e - NR0;
             v = weights(*reinterpret_cast<const stg_t *>(wlrows[r] + min(x, W - 1) * TP + 4 * q));
-            slot = RING + x % LRING;
+            slot = RING + x % (DL ? 1 : LRING);
         }
         ring[(r * ROWE + slot) * Q + q] = v;
     }
@@ -561,7 +436,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
         if constexpr (s % K == 0) {
             // top of a batch (steps [x, x+K)): write the entries the next batch reads
             // first (loaded a batch ago), then load the ones after them
-            f4 wv[SPL];  // (IDX: every share's LUT reads before the first ring write)
+            f4 wv[SPL];
 #pragma unroll
             for (int j = 0; j < SPL; ++j) wv[j] = weights(stg[j]);
 #pragma unroll
@@ -614,9 +489,9 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 // ---------------------------------------------------------------------------
 // launchers (one (T, DM) per translation unit: build/p32_t<T>_d<DM>.hip)
 // ---------------------------------------------------------------------------
-template <int T, int NW, int DM, int CP, int NPH, bool IDX = false, bool C16 = false, bool OTF = false>
+template <int T, int NW, int DM, int CP, int NPH, bool C16 = false>
 void launch_v32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
-                hipStream_t st, const float *lut = nullptr) {
+                hipStream_t st) {
     constexpr int U = pf9_period(T);
     const int W = p->width, H = p->height;
     const int nxb = (W + 2 * NW - 1) / (2 * NW);
@@ -633,30 +508,23 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
     const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
     nstrip = (H + rows - 1) / rows;
     const int per_xcd = (nxb + 7) / 8;
-    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, IDX, 2, 4, C16, OTF>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0,
-                       st, wl, wr, cin, cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd, lut);
-    note_pass_kernel(ASW_DIR_V, DM, OTF ? "k_vpass32_otf" : C16 ? "k_vpass32_c16" : "k_vpass32", T,
-                     NW == 16 ? (NPH == 4 ? (IDX ? "NW=16,NPH=4,IDX" : "NW=16,NPH=4") : (IDX ? "NW=16,IDX" : "NW=16"))
-                              : "NW=8,NPH=3",
-                     CP == kCPStream);
+    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, 2, 4, C16>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl,
+                       wr, cin, cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd);
+    note_pass_kernel(ASW_DIR_V, DM, C16 ? "k_vpass32_c16" : "k_vpass32", T,
+                     NW == 16 ? (NPH == 4 ? "NW=16,NPH=4" : "NW=16") : "NW=8,NPH=3", CP == kCPStream);
 }
 
-template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, bool IDX = false, int KB = 0,
-          bool DL = false>
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, int KB = 0, bool DL = false>
 void launch_h32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
-                hipStream_t st, int seg_len, const float *lut = nullptr) {
+                hipStream_t st, int seg_len) {
     const int W = p->width, H = p->height;
     const int nseg = (W + seg_len - 1) / seg_len;
     const int npairs = (H + 1) / 2 * nseg;  // work items: (row pair, segment)
     const int per_xcd = (npairs + 7) / 8;
     const int blocks_per_xcd = (per_xcd + NWB - 1) / NWB;
-    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE, IDX, KB, DL>), dim3(8 * blocks_per_xcd),
-                       dim3(NWB * 64), 0, st, wl, wr, cin, cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd,
-                       lut);
-    char shape[48];
-    std::snprintf(shape, sizeof shape, "NWB=%d,NPH=%d%s", NWB, NPH, IDX ? ",IDX" : "");
-    note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T,
-                     IDX ? shape : DL ? "NWB=1,NPH=4,DL" : NPH == 4 ? "NWB=1,NPH=4" : NWB == 4 ? "NWB=4" : "NWB=2",
+    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE, KB, DL>), dim3(8 * blocks_per_xcd), dim3(NWB * 64),
+                       0, st, wl, wr, cin, cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd);
+    note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T, DL ? "NWB=1,NPH=4,DL" : NWB == 4 ? "NWB=4" : "NWB=2",
                      CP == kCPStream);
 }
 
@@ -687,49 +555,32 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         if (stream) launch_v32<T, NW, DM, kCPStream, NPH>(p, wl, wr, cin, cout, den, st);
         else launch_v32<T, NW, DM, 0, NPH>(p, wl, wr, cin, cout, den, st);
     } else {
-        // segments per row pair: as many as keep the waves within one round of the
-        // 2048 wave slots (8 per CU: two 4-wave blocks of 67 KB LDS) — at C4 three
-        // 640-column segments, 1620 waves (four segments, 2160 waves, left a tail round
-        // of 112 waves); the window prologue (U-1 columns) is paid once per segment.
-        // Variant bits 20-23 (asw_tune_set) override the segment count.
-        // T <= 35: the "lean" form, 4 weight phases in one-wave blocks (138 VGPRs, up to
-        // 9-11 waves per CU against 8): C4 / 8 den-read 0.326 against 0.358 ms
-        // (profiles/r04/pass32_h_r09e.log).  Variant
-        // bit 24 selects the 4-wave-block form instead.
-        const bool lean = T <= 35 && !(g_pass_variant & (1 << 24));
-        // the lean form with its left weights from DPP rows (DL) by default: in the C4 / 8
-        // frame 0.325 against 0.355 ms per pass under rocprofv3, shard frame 4.71-4.74
-        // against 4.74-4.88 ms (round 5, profiles/r05/kernel_stats_r12q_shard8_hdl.csv,
-        // shard_hdl_r12q.log); variant bit 27 selects the left ring in LDS instead
-        const bool dl = lean && !(g_pass_variant & (1 << 27));
+        // T <= 35: the "lean" form, 4 weight phases in one-wave blocks (up to 11 waves per
+        // CU against 8 for 4-wave blocks; C4 / 8 den-read 0.326 against 0.358 ms,
+        // profiles/r04/pass32_h_r09e.log), the conflict-free 48-entry right ring (C4 8-way
+        // shard frame 4.73 against 4.81-4.98 ms with the minimal 40-entry ring,
+        // profiles/r04/shard_variants_r11g.log) and the left weights from DPP rows (DL: in
+        // the C4 / 8 frame 0.325 against 0.355 ms per pass under rocprofv3, shard frame
+        // 4.71-4.74 against 4.74-4.88 ms with the left ring in LDS, round 5,
+        // profiles/r05/kernel_stats_r12q_shard8_hdl.csv, shard_hdl_r12q.log).  Segments per
+        // row pair sized to the 11 wave slots per CU its LDS admits (C4: 5 segments of 384
+        // columns); the window prologue (U-1 columns) is paid once per segment.  Variant
+        // bits 20-23 (asw_tune_set) override the segment count.
+        // T > 35: 2-wave blocks, 2 weight phases.
         const int pairs = (p->height + 1) / 2;
-        // (DL: the wave slots its LDS admits, 11 per CU against 9 with the left ring;
-        // C4: 5 segments of 384 columns)
-        const int slots = dl ? 256 * 11 : 2048;
-        int nseg = (slots + pairs / 2) / (pairs > 0 ? pairs : 1);  // C4: 4 segments of 480 columns
+        const int slots = T <= 35 ? 256 * 11 : 2048;
+        int nseg = (slots + pairs / 2) / (pairs > 0 ? pairs : 1);
         if ((g_pass_variant >> 20) & 15) nseg = (g_pass_variant >> 20) & 15;
         if (nseg < 1) nseg = 1;
         int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
         if (seg < 2 * U) seg = 2 * U;
-        constexpr int NWB = T > 35 ? 2 : 4;
         if constexpr (T <= 35) {
-            if (dl) {
-                if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
-                else launch_h32<T, 1, DM, 0, 4, true, 3, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
-                return finish32();
-            }
-            if (lean) {
-                // (one-wave blocks with the conflict-free 48-entry ring, 16.7 KB of LDS, 9 per
-                // CU: C4 8-way shard frame 4.73 against 4.81-4.98 ms with the minimal 40-entry
-                // ring, 14.4 KB, 11 per CU, profiles/r04/shard_variants_r11g.log; the minimal
-                // ring's lean form is no longer built, round 5)
-                if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
-                else launch_h32<T, 1, DM, 0, 4, true, 3>(p, wl, wr, cin, cout, den, st, seg);
-                return finish32();
-            }
+            if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+            else launch_h32<T, 1, DM, 0, 4, true, 3, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+        } else {
+            if (stream) launch_h32<T, 2, DM, kCPStream, 2>(p, wl, wr, cin, cout, den, st, seg);
+            else launch_h32<T, 2, DM, 0, 2>(p, wl, wr, cin, cout, den, st, seg);
         }
-        if (stream) launch_h32<T, NWB, DM, kCPStream, 2>(p, wl, wr, cin, cout, den, st, seg);
-        else launch_h32<T, NWB, DM, 0, 2>(p, wl, wr, cin, cout, den, st, seg);
     }
     return finish32();
 }
@@ -747,93 +598,14 @@ int launch_pass32_c16_tm(const asw_params *p, const float *wl, const float *wr, 
         bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
         if (g_pass_variant & (1 << 26)) stream = !stream;
         const float *c = reinterpret_cast<const float *>(cin16);
-        if (stream) launch_v32<T, NW, DM, kCPStream, NPH, false, true>(p, wl, wr, c, cout, den, st);
-        else launch_v32<T, NW, DM, 0, NPH, false, true>(p, wl, wr, c, cout, den, st);
-        return finish32();
-    }
-}
-
-// the V pass with both weights on the fly (asw_aggregate_pass_otf_v): T <= 35 (16-wave
-// blocks), den mode NONE (what a 32-plane shard's V passes run)
-template <int T>
-int launch_pass32_otf_v_t(const asw_params *p, const uint8_t *left, const uint8_t *right, const float *lut,
-                          const float *cin, float *cout, hipStream_t st) {
-    if constexpr (T > 35) {
-        return ASW_E_UNSUPPORTED;
-    } else {
-        constexpr int NPH = T >= 33 ? 4 : 2;
-        bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
-        if (g_pass_variant & (1 << 26)) stream = !stream;
-        const float *l = reinterpret_cast<const float *>(left), *r = reinterpret_cast<const float *>(right);
-        if (stream) launch_v32<T, 16, DM_NONE, kCPStream, NPH, false, false, true>(p, l, r, cin, cout, nullptr, st, lut);
-        else launch_v32<T, 16, DM_NONE, 0, NPH, false, false, true>(p, l, r, cin, cout, nullptr, st, lut);
-        return finish32();
-    }
-}
-
-// the V pass over index-form supports (asw_aggregate_pass_index): 16-wave blocks
-// (T <= 35; their slab ring and the (R+1) x 766 LUT fit the 160 KB LDS), den mode
-// NONE (what a 32-plane shard's V passes run)
-// H over index-form supports: blocks of 8 waves share one LDS copy of the LUT (55 KB
-// at T = 35) beside their 8 private rings of the minimal length at refill batches of 2
-// steps (8 x 12 KB): 8 waves per CU, against up to 11 one-wave blocks of the float form.
-template <int T, int DM, int CP>
-void launch_h32_idx(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
-                    hipStream_t st, const float *lut) {
-    constexpr int U = pf9_period(T);
-    const int pairs = (p->height + 1) / 2;
-    int nseg = (2048 + pairs / 2) / (pairs > 0 ? pairs : 1);
-    if ((g_pass_variant >> 20) & 15) nseg = (g_pass_variant >> 20) & 15;
-    if (nseg < 1) nseg = 1;
-    int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
-    if (seg < 2 * U) seg = 2 * U;
-    constexpr int NPH = T >= 33 ? 4 : 2;
-    if (g_pass_variant & (1 << 25))  // (variant bit 25: two weight phases, more registers)
-        launch_h32<T, 8, DM, CP, 2, false, 2, true, 2>(p, wl, wr, cin, cout, den, st, seg, lut);
-    else launch_h32<T, 8, DM, CP, NPH, false, 2, true, 2>(p, wl, wr, cin, cout, den, st, seg, lut);
-}
-
-template <int T>
-int launch_pass32_idx_tm(const asw_params *p, int dir, const uint16_t *wl, const uint16_t *wr, const float *lut,
-                         const float *cin, float *cout, float *den, int dm, hipStream_t st) {
-    if constexpr (T > 35) {
-        return ASW_E_UNSUPPORTED;
-    } else {
-        constexpr int NPH = T >= 33 ? 4 : 2;
-        const bool stream = (long long)p->width * p->height * kPlanes32 * 4 >= (256LL << 20);
-        const float *l = reinterpret_cast<const float *>(wl), *r = reinterpret_cast<const float *>(wr);
-        if (dir == ASW_DIR_V) {
-            if (dm != ASW_DEN_NONE) return ASW_E_UNSUPPORTED;
-            if (stream) launch_v32<T, 16, DM_NONE, kCPStream, NPH, true>(p, l, r, cin, cout, nullptr, st, lut);
-            else launch_v32<T, 16, DM_NONE, 0, NPH, true>(p, l, r, cin, cout, nullptr, st, lut);
-        } else {
-            // (every den mode in this one translation unit: the Makefile instantiates the
-            // index passes once per tap count)
-            if (stream) {
-                if (dm == ASW_DEN_READ) launch_h32_idx<T, DM_READ, kCPStream>(p, l, r, cin, cout, den, st, lut);
-                else if (dm == ASW_DEN_WRITE) launch_h32_idx<T, DM_WRITE, kCPStream>(p, l, r, cin, cout, den, st, lut);
-                else launch_h32_idx<T, DM_NONE, kCPStream>(p, l, r, cin, cout, den, st, lut);
-            } else {
-                if (dm == ASW_DEN_READ) launch_h32_idx<T, DM_READ, 0>(p, l, r, cin, cout, den, st, lut);
-                else if (dm == ASW_DEN_WRITE) launch_h32_idx<T, DM_WRITE, 0>(p, l, r, cin, cout, den, st, lut);
-                else launch_h32_idx<T, DM_NONE, 0>(p, l, r, cin, cout, den, st, lut);
-            }
-        }
+        if (stream) launch_v32<T, NW, DM, kCPStream, NPH, true>(p, wl, wr, c, cout, den, st);
+        else launch_v32<T, NW, DM, 0, NPH, true>(p, wl, wr, c, cout, den, st);
         return finish32();
     }
 }
 
 }  // namespace agg
 }  // namespace asw
-
-#define ASW_INSTANTIATE_PASS32_OTF_V(TT)                                                                          \
-    template int asw::agg::launch_pass32_otf_v_t<TT>(const asw_params *, const uint8_t *, const uint8_t *,        \
-                                                     const float *, const float *, float *, hipStream_t);
-
-#define ASW_INSTANTIATE_PASS32_IDX(TT)                                                                            \
-    template int asw::agg::launch_pass32_idx_tm<TT>(const asw_params *, int, const uint16_t *, const uint16_t *, \
-                                                    const float *, const float *, float *, float *, int, hipStream_t); \
-    ASW_INSTANTIATE_PASS32_OTF_V(TT)
 
 #define ASW_INSTANTIATE_PASS32(TT, DM)                                                                            \
     template int asw::agg::launch_pass32_tm<TT, DM>(const asw_params *, int, const float *, const float *,       \

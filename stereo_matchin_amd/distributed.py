@@ -106,13 +106,12 @@ class HipShardOps:
 class ShardedStereoMatcher:
     """One rank's share of a d-sharded frame."""
 
-    def __init__(self, params: AswParams, rank: int, world: int, device="cuda", group=None,
-                 support_index: bool | None = None):
+    def __init__(self, params: AswParams, rank: int, world: int, device="cuda", group=None):
         p = params.copy()
         p.d_begin, p.d_end = shard_range(params.ndisp, rank, world)
         self.p = p
         self.rank, self.world = rank, world
-        self.matcher = StereoMatcher(p, device, support_index=support_index)
+        self.matcher = StereoMatcher(p, device)
         self.ops = HipShardOps(p)
         self.reduce_min = _allreduce_min_factory(group)
 
@@ -120,11 +119,10 @@ class ShardedStereoMatcher:
         m = self.matcher
         if events is not None:
             events.append(("start", _record()))
-        fuse = m.fuse_raw and self.p.iters >= 1  # asw_Aggr fused into the first V pass
-        m.raw_and_support(left, right, raw=not fuse)
+        m.raw_and_support(left, right)
         if events is not None:
             events.append(("support", _record()))
-        cost = m.aggregate(events, images=(left, right) if fuse else None)
+        cost = m.aggregate(events)
         # (m.local: the local scan, when the last pass ran it)
         d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = sharded_wta(self.ops, cost, self.reduce_min, m.local)
         if events is not None:
@@ -196,25 +194,24 @@ class PipelinedMatcher:
         m = st.matcher if self.sharded else st
         if events is not None:
             events.append(("start", _record()))
-        fuse = m.fuse_raw and m.p.iters >= 1
         if self.overlap_prep:
             # raw cost + supports of this frame on the prep stream, after set i's previous
             # tail (its last reader), beside whatever the main stream is running
             if self.done[i] is not None:
                 self.prep.wait_event(self.done[i])
             with torch.cuda.stream(self.prep):
-                m.raw_and_support(left, right, raw=not fuse)
+                m.raw_and_support(left, right)
                 prepared = torch.cuda.Event()
                 prepared.record(self.prep)
             for t in (left, right):
                 t.record_stream(self.prep)
             main.wait_event(prepared)
         else:
-            m.raw_and_support(left, right, raw=not fuse)
+            m.raw_and_support(left, right)
         if events is not None:
             events.append(("support", _record()))
-        cost = m.aggregate(events, images=(left, right) if fuse else None)
-        local = m.local  # the local scan, when the last pass ran it (wta_fused)
+        cost = m.aggregate(events)
+        local = m.local  # the local scan, when a pass already ran it
         if local is None and self.sharded:
             local = st.ops.local(cost)
         ready = torch.cuda.Event()

@@ -84,28 +84,6 @@ def asw_Aggr(p: AswParams, left: torch.Tensor, right: torch.Tensor, out: torch.T
     return out
 
 
-def otf_v_supported(p: AswParams) -> bool:
-    """asw_pass_otf_v_supported: a 32-plane shard's V pass can compute both weights on the fly."""
-    return bool(_lib.lib().asw_pass_otf_v_supported(ctypes.byref(p)))
-
-
-def asw_vCostAggregation_otf_v(p: AswParams, left: torch.Tensor, right: torch.Tensor, lut: torch.Tensor, cost_in,
-                               out=None):
-    """The V pass of a 32-plane shard with both support weights computed on the fly from
-    the images and the LUT (asw_aggregate_pass_otf_v), den mode NONE:
-    bit-identical to asw_vCostAggregation(p, asw_vSupport(p, left), asw_vSupport(p, right), ...)."""
-    _expect(left, (p.height, p.width, 4), torch.uint8, "left")
-    _expect(right, (p.height, p.width, 4), torch.uint8, "right")
-    _expect(lut, lut_shape(p), torch.float32, "lut")
-    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
-    if out is None:
-        out = new_cost(p, cost_in.device)
-    _expect(out, cost_shape(p), torch.float32, "out")
-    _lib.check(_lib.lib().asw_aggregate_pass_otf_v(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(lut), _ptr(cost_in),
-                                                   _ptr(out), _stream(cost_in.device)), "asw_aggregate_pass_otf_v")
-    return out
-
-
 def raw16_supported(p: AswParams) -> bool:
     """asw_raw16_supported: the uint16 raw-cost volume (asw_raw_cost16) and the first V
     pass over it (asw_aggregate_pass_den16) are built for p."""
@@ -171,59 +149,15 @@ def _support(p: AswParams, direction: int, img: torch.Tensor, lut: torch.Tensor 
     return out
 
 
-def new_support_index(p: AswParams, device) -> torch.Tensor:
-    """A support array in index form: uint16 LUT indices [H][W][Tp] (torch has no
-    uint16 arithmetic on every build: int16 storage of the same bits)."""
-    return torch.empty(support_shape(p), dtype=torch.int16, device=device)
-
-
 def support_all(p: AswParams, left: torch.Tensor, right: torch.Tensor, lut: torch.Tensor, wvl: torch.Tensor,
                 whl: torch.Tensor, wvr: torch.Tensor, whr: torch.Tensor) -> None:
-    """asw_vSupport + asw_hSupport of both images in one launch (``asw_support_all``).
-
-    An int16 tensor (``new_support_index``) receives that array in index form
-    (``asw_support_all_fmt``): the LUT index of each weight, lut[index] = the weight."""
+    """asw_vSupport + asw_hSupport of both images in one launch (``asw_support_all``)."""
     for img in (left, right):
         _expect(img, (p.height, p.width, 4), torch.uint8, "image")
-    mask = 0
-    for j, w in enumerate((wvl, whl, wvr, whr)):
-        if w is None:  # not computed (e.g. whr with the on-the-fly H pass)
-            continue
-        if w.dtype == torch.int16:
-            mask |= 1 << j
-            _expect(w, support_shape(p), torch.int16, "out")
-        else:
-            _expect(w, support_shape(p), torch.float32, "out")
-    _lib.check(_lib.lib().asw_support_all_fmt(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(lut), _ptr(wvl),
-                                              _ptr(whl), _ptr(wvr), _ptr(whr), mask, _stream(left.device)),
-               "asw_support_all_fmt")
-
-
-def index_supported(p: AswParams, direction: int = DIR_V, den_mode: int = 0) -> bool:
-    """asw_pass_index_supported: a pass of (direction, den_mode) reads index-form supports."""
-    return bool(_lib.lib().asw_pass_index_supported(ctypes.byref(p), direction, den_mode))
-
-
-def aggregate_pass_index(p: AswParams, direction: int, supp_left, supp_right, lut, cost_in, out=None, den=None,
-                         den_mode: int = 0):
-    """One aggregation pass over index-form supports (asw_aggregate_pass_index):
-    bit-identical to the pass over the float arrays (lut[index] = the weight)."""
-    _expect(supp_left, support_shape(p), torch.int16, "supp_left")
-    _expect(supp_right, support_shape(p), torch.int16, "supp_right")
-    _expect(lut, lut_shape(p), torch.float32, "lut")
-    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
-    if out is None:
-        out = torch.empty_like(cost_in)
-    _expect(out, cost_shape(p), torch.float32, "out")
-    if out.data_ptr() == cost_in.data_ptr():
-        raise ValueError("aggregation passes are out of place (cost_in != out)")
-    if den_mode:
-        _expect(den, cost_shape(p), torch.float32, "den")
-    _lib.check(_lib.lib().asw_aggregate_pass_index(ctypes.byref(p), direction, _ptr(supp_left), _ptr(supp_right),
-                                                   _ptr(lut), _ptr(cost_in), _ptr(out), _ptr(den), den_mode,
-                                                   _stream(cost_in.device)),
-               "asw_aggregate_pass_index")
-    return out
+    for w in (wvl, whl, wvr, whr):
+        _expect(w, support_shape(p), torch.float32, "out")
+    _lib.check(_lib.lib().asw_support_all(ctypes.byref(p), _ptr(left), _ptr(right), _ptr(lut), _ptr(wvl), _ptr(whl),
+                                          _ptr(wvr), _ptr(whr), _stream(left.device)), "asw_support_all")
 
 
 def lab_image(p: AswParams, img: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -275,34 +209,6 @@ def _pass(p: AswParams, direction: int, supp_left, supp_right, cost_in, out, den
     return out
 
 
-def otf_supported(p: AswParams, direction: int = DIR_H) -> bool:
-    """asw_pass_otf_supported: the pass can compute its right weights on the fly."""
-    return bool(_lib.lib().asw_pass_otf_supported(ctypes.byref(p), direction))
-
-
-def asw_hCostAggregation_otf(p: AswParams, supp_left, right: torch.Tensor, lut: torch.Tensor, cost_in, out=None,
-                             den=None, den_mode: int = 0):
-    """The H pass with the right support weights computed on the fly from the right
-    image and the LUT (asw_aggregate_pass_otf): bit-identical to
-    asw_hCostAggregation(p, supp_left, asw_hSupport(p, right), ...)."""
-    _expect(supp_left, support_shape(p), torch.float32, "supp_left")
-    _expect(right, (p.height, p.width, 4), torch.uint8, "right")
-    _expect(lut, lut_shape(p), torch.float32, "lut")
-    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
-    if out is None:
-        out = torch.empty_like(cost_in)
-    _expect(out, cost_shape(p), torch.float32, "out")
-    if out.data_ptr() == cost_in.data_ptr():
-        raise ValueError("aggregation passes are out of place (cost_in != out)")
-    if den_mode:
-        _expect(den, cost_shape(p), torch.float32, "den")
-    _lib.check(_lib.lib().asw_aggregate_pass_otf(ctypes.byref(p), DIR_H, _ptr(supp_left), _ptr(right), _ptr(lut),
-                                                 _ptr(cost_in), _ptr(out), _ptr(den), den_mode,
-                                                 _stream(cost_in.device)),
-               "asw_aggregate_pass_otf")
-    return out
-
-
 def pass_kernel(direction: int, den_mode: int) -> str | None:
     """Name of the kernel instantiation the latest aggregation-pass launch of
     (direction, den_mode) in this process ran (asw_pass_kernel), or None."""
@@ -321,72 +227,15 @@ def asw_vCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None,
     return _pass(p, DIR_V, supp_left, supp_right, cost_in, out, den, den_mode)
 
 
-def raw_fused_supported(p: AswParams) -> bool:
-    """asw_pass_raw_supported: asw_aggregate_pass_raw is built for p (ring tap counts of
-    this library build, not a 32-plane shard, r >= 1)."""
-    return bool(_lib.lib().asw_pass_raw_supported(ctypes.byref(p)))
-
-
-def asw_vCostAggregation_raw(p: AswParams, supp_left, supp_right, left, right, out=None, den=None,
-                             den_mode: int = 0):
-    """The first vertical pass with asw_Aggr fused (K/asw_aggr.cl:3-23 then
-    K/asw_vcost_aggregation.cl:11-44): the window's raw costs come from the images,
-    no raw-cost volume.  Same result as ``asw_vCostAggregation(asw_Aggr(...))``."""
-    _expect(supp_left, support_shape(p), torch.float32, "supp_left")
-    _expect(supp_right, support_shape(p), torch.float32, "supp_right")
-    _expect(left, (p.height, p.width, 4), torch.uint8, "left")
-    _expect(right, (p.height, p.width, 4), torch.uint8, "right")
-    if out is None:
-        out = new_cost(p, left.device)
-    _expect(out, cost_shape(p), torch.float32, "out")
-    if den_mode:
-        _expect(den, cost_shape(p), torch.float32, "den")
-    _lib.check(_lib.lib().asw_aggregate_pass_raw(ctypes.byref(p), _ptr(supp_left), _ptr(supp_right), _ptr(left),
-                                                 _ptr(right), _ptr(out), _ptr(den), den_mode, _stream(left.device)),
-               "asw_aggregate_pass_raw")
-    return out
-
-
 def asw_hCostAggregation(p: AswParams, supp_left, supp_right, cost_in, out=None, den=None, den_mode: int = 0):
     """One horizontal weighted-aggregation pass (K/asw_hcost_aggregation.cl:12-44)."""
     return _pass(p, DIR_H, supp_left, supp_right, cost_in, out, den, den_mode)
 
 
-def wta_local_fused_supported(p: AswParams) -> bool:
-    """asw_pass_wta_local_supported: the den-read H pass of this context can run the
-    WTA's own scan fused (asw_aggregate_pass_wta_local)."""
-    return bool(_lib.lib().asw_pass_wta_local_supported(ctypes.byref(p)))
-
-
-def asw_hCostAggregation_wta_local(p: AswParams, supp_left, supp_right, cost_in, den, out=None, key=None, m1=None,
-                                   m2=None):
-    """The last horizontal pass, den-read, with the local WTA scan fused
-    (asw_aggregate_pass_wta_local): ``out`` is asw_hCostAggregation's output and
-    ``(key, m1, m2)`` equal :func:`wta_local` on it.  Returns ``(out, key, m1, m2)``."""
-    _expect(cost_in, cost_shape(p), torch.float32, "cost_in")
-    _expect(den, cost_shape(p), torch.float32, "den")
-    _expect(supp_left, support_shape(p), torch.float32, "supp_left")
-    _expect(supp_right, support_shape(p), torch.float32, "supp_right")
-    dev = cost_in.device
-    H, W = p.height, p.width
-    out = new_cost(p, dev) if out is None else out
-    key = torch.empty((H, W), dtype=torch.int64, device=dev) if key is None else key
-    m1 = torch.empty((H, W), dtype=torch.float32, device=dev) if m1 is None else m1
-    m2 = torch.empty((H, W), dtype=torch.float32, device=dev) if m2 is None else m2
-    _expect(out, cost_shape(p), torch.float32, "out")
-    _expect(key, (H, W), torch.int64, "key")
-    _expect(m1, (H, W), torch.float32, "m1")
-    _expect(m2, (H, W), torch.float32, "m2")
-    _lib.check(_lib.lib().asw_aggregate_pass_wta_local(ctypes.byref(p), _ptr(supp_left), _ptr(supp_right),
-                                                       _ptr(cost_in), _ptr(out), _ptr(den), _ptr(key), _ptr(m1),
-                                                       _ptr(m2), _stream(dev)), "asw_aggregate_pass_wta_local")
-    return out, key, m1, m2
-
-
 def wta_from_local(p: AswParams, cost, key, m1, m2):
-    """asw_WTA's outputs on a whole-range volume from its local scan (key, m1, m2; e.g. of
-    asw_hCostAggregation_wta_local): the one-shard case of the d-sharded protocol, the
-    target scan and the finalize (one shard's second minima are its own)."""
+    """asw_WTA's outputs on a whole-range volume from its local scan (key, m1, m2): the
+    one-shard case of the d-sharded protocol, the target scan and the finalize (one
+    shard's second minima are its own)."""
     tkey, t1, t2 = wta_target_local(p, cost, key)
     return wta_finalize(p, key, m2, tkey, t2)
 

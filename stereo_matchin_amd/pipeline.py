@@ -48,104 +48,40 @@ class StereoMatcher:
     (V, H) as volumes — written by the first pass of each direction, read by the
     other r-1 (ASW_DEN_*); bit-identical results, 2 more cost-sized buffers."""
 
-    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True, fuse_raw: bool | None = None,
-                 otf: bool | None = None, support_index: bool | str | None = None, otf_v: bool | None = None,
-                 wta_fused: bool | None = None):
+    def __init__(self, params: AswParams, device="cuda", den_cache: bool = True):
         st = _lib.params_check(params)
         if st != _lib.ASW_OK:
             raise _lib.AswError(st, "asw_params_check")
         self.p = params.copy()
-        # asw_Aggr fused into the first V pass (k_vpass10_raw, asw_aggregate_pass_raw): the
-        # raw-cost volume is never written nor read; bit-identical, measured slower at C4
-        # (2.40 ms against 0.37 + 1.78, profiles/r04/fused_raw_r10d.log).  Default (None):
-        # params.flags & ASW_FLAG_FUSE_RAW (where built: ring tap counts, not a 32-plane shard)
-        if fuse_raw is None:
-            fuse_raw = bool(params.flags & _lib.FLAG_FUSE_RAW)
-        self.fuse_raw = bool(fuse_raw) and K.raw_fused_supported(self.p)
         self.device = torch.device(device)
         dev = self.device
         self.lut = torch.empty(K.lut_shape(self.p), dtype=torch.float32, device=dev)
-        # otf: the H passes compute their right support weights from the right image
-        # (asw_aggregate_pass_otf), so whr is never built.  Off by default: bit-identical
-        # but measured slower (C4 H den-read 2.30 against 1.42 ms: the refill pipeline's
-        # registers cost the pass its latency cover; DESIGN.md §On-the-fly supports)
-        if otf is None:
-            otf = bool(params.flags & _lib.FLAG_OTF_H)
-        self.otf = bool(otf) and K.otf_supported(self.p)
-        # otf: a matcher-owned copy of the right image (the H passes read it after
-        # raw_and_support returns; the caller's buffer may be reused by then)
-        # otf_v (a 32-plane shard, SURVEY §8(f)3): the V passes compute both weights from
-        # the images and the LUT (asw_aggregate_pass_otf_v), so wvl / wvr are never built.
-        # Default (None): params.flags & ASW_FLAG_OTF_V, as asw_create reads it
-        if otf_v is None:
-            otf_v = bool(params.flags & _lib.FLAG_OTF_V)
-        self.otfv = bool(otf_v) and K.otf_v_supported(self.p)
-        self.right = torch.empty((self.p.height, self.p.width, 4), dtype=torch.uint8, device=dev) \
-            if self.otf or self.otfv else None
-        self.left = torch.empty((self.p.height, self.p.width, 4), dtype=torch.uint8, device=dev) \
-            if self.otfv else None
-        # support_index (opt-in, where built: a 32-plane shard's passes): the supports in
-        # index form, uint16 LUT indices (asw_support_all_fmt), half the bytes of the
-        # replicated support stream; asw_aggregate_pass_index reads them.  "v": the V
-        # passes only.  Bit-identical, measured slower (C4 / 8: V 0.351 against 0.265 ms,
-        # H 0.68 against 0.36; the passes are LDS-bound and the LUT reads cost more LDS
-        # cycles than the halved bytes save; DESIGN.md §Support stream)
-        want = support_index
-        if want is None:  # the context flags (ASW_FLAG_SUPPORT_INDEX / _V), as asw_create reads them
-            want = True if params.flags & _lib.FLAG_SUPPORT_INDEX else \
-                "v" if params.flags & _lib.FLAG_SUPPORT_INDEX_V else False
-        self.vidx = bool(want) and not self.otfv and K.index_supported(self.p, DIR_V, _lib.DEN_NONE)
-        self.hidx = self.vidx and want != "v" and not self.otf and K.index_supported(self.p, DIR_H, _lib.DEN_READ)
-        new_v = K.new_support_index if self.vidx else K.new_support
-        new_h = K.new_support_index if self.hidx else K.new_support
-        self.wvl = None if self.otfv else new_v(self.p, dev)
-        self.wvr = None if self.otfv else new_v(self.p, dev)
-        self.whl = new_h(self.p, dev)
-        self.whr = None if self.otf else new_h(self.p, dev)
+        self.wvl, self.wvr, self.whl, self.whr = (K.new_support(self.p, dev) for _ in range(4))
         self.c0 = K.new_cost(self.p, dev)
         self.c1 = K.new_cost(self.p, dev)
         # the raw costs as uint16 in c0's first half (asw_raw_cost16 + the first V pass
         # asw_aggregate_pass_den16: half the bytes of asw_Aggr's write and that pass's read,
-        # bit-identical), unless fused or index-form (ASW_FLAG_RAW_F32 keeps the float volume)
-        self.raw16 = (not self.fuse_raw and not self.vidx and not self.otfv and not params.flags & _lib.FLAG_RAW_F32
-                      and K.raw16_supported(self.p))
+        # bit-identical); ASW_FLAG_RAW_F32 keeps the float volume
+        self.raw16 = not params.flags & _lib.FLAG_RAW_F32 and K.raw16_supported(self.p)
         self.c0_16 = K.cost16_view(self.c0) if self.raw16 else None
         self.den_v = self.den_h = None
-        if den_cache and self.p.iters >= 2:
+        if den_cache and self.p.iters >= 2 and K.cost_shape(self.p)[2] != 32:
             # a 32-plane shard's passes recompute den (C4 / 8: k_vpass32 den-none 0.24
             # against den-read 0.28 ms, k_hpass32 0.30-0.33 against 0.36,
-            # profiles/r04/h32_variants_r11d.log; ASW_FLAG_SHARD_DEN_H keeps the H pass
-            # reading it; asw_frame.cpp the same)
-            p32 = K.cost_shape(self.p)[2] == 32
-            if not p32:
-                self.den_v = K.new_cost(self.p, dev)
-            if not p32 or params.flags & _lib.FLAG_SHARD_DEN_H:
-                self.den_h = K.new_cost(self.p, dev)
-        # wta_fused: the WTA's own scan runs inside the last H pass (asw_aggregate_pass_wta_local:
-        # a den-read k_hpass11 with one block over every plane), so the WTA does not re-read
-        # the volume for it; aggregate() leaves the scan's key / m1 / m2 in self.local, and
-        # match() / the sharded protocol take them from there.  Bit-identical, measured
-        # slower at C4 (23.02-23.06 against 22.95 ms: the fused pass runs at 3 blocks per CU,
-        # profiles/r05/bench_f1_r12t.log), so opt-in: default (None) params.flags &
-        # ASW_FLAG_WTA_FUSED, as asw_create reads it
-        if wta_fused is None:
-            wta_fused = bool(params.flags & _lib.FLAG_WTA_FUSED)
-        self.wta_fused = (bool(wta_fused) and not self.otf and not self.hidx and self.den_h is not None
-                          and self.p.iters >= 2 and K.wta_local_fused_supported(self.p))
-        H, W = self.p.height, self.p.width
+            # profiles/r04/h32_variants_r11d.log; asw_frame.cpp the same)
+            self.den_v = K.new_cost(self.p, dev)
+            self.den_h = K.new_cost(self.p, dev)
+        # the WTA's local scan (key, m1, m2) of c0 when a pass already produced it (None:
+        # asw_WTA / asw_wta_local scan the volume); read by match() and the d-sharded protocol
         self.local = None
-        self._local_bufs = (torch.empty((H, W), dtype=torch.int64, device=dev),
-                            torch.empty((H, W), dtype=torch.float32, device=dev),
-                            torch.empty((H, W), dtype=torch.float32, device=dev)) if self.wta_fused else None
 
     # -- stages ---------------------------------------------------------------
-    def raw_and_support(self, left: torch.Tensor, right: torch.Tensor, raw: bool = True):
-        """asw_Aggr into c0 (unless ``raw`` is False: the first V pass computes it,
-        see ``aggregate(images=...)``) and the four support arrays."""
+    def raw_and_support(self, left: torch.Tensor, right: torch.Tensor):
+        """asw_Aggr into c0 and the four support arrays."""
         p = self.p
-        if raw and self.raw16:
+        if self.raw16:
             K.asw_Aggr16(p, left, right, out=self.c0_16)
-        elif raw:
+        else:
             K.asw_Aggr(p, left, right, out=self.c0)
         if p.color_space == COLOR_LAB:
             lab_l, lab_r = K.lab_image(p, left), K.lab_image(p, right)
@@ -156,48 +92,22 @@ class StereoMatcher:
             return
         K.support_lut(p, self.device, out=self.lut)
         # asw_vSupport / asw_hSupport of both images (main.cpp:469-484) in one launch
-        # (without asw_hSupport(right) when the H passes compute it on the fly)
         K.support_all(p, left, right, self.lut, self.wvl, self.whl, self.wvr, self.whr)
-        if self.otf or self.otfv:
-            self.right.copy_(right.reshape(self.right.shape))
-        if self.otfv:
-            self.left.copy_(left.reshape(self.left.shape))
 
-    def aggregate(self, events: list | None = None, images: tuple | None = None):
-        """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515).
-        ``images`` = (left, right): the first V pass computes the raw cost itself
-        (asw_aggregate_pass_raw) and c0's input content is not used.  With ``wta_fused``
-        the last H pass also leaves the WTA's local scan of c0 in ``self.local``."""
+    def aggregate(self, events: list | None = None):
+        """r x (V: c0 -> c1, H: c1 -> c0); the result is in c0 (main.cpp:486-515)."""
         p = self.p
         self.local = None
         for it in range(p.iters):
             dmv = _lib.DEN_NONE if self.den_v is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
             dm = _lib.DEN_NONE if self.den_h is None else (_lib.DEN_WRITE if it == 0 else _lib.DEN_READ)
-            if it == 0 and images is not None:
-                K.asw_vCostAggregation_raw(p, self.wvl, self.wvr, images[0], images[1], out=self.c1, den=self.den_v,
-                                           den_mode=dmv)
-            elif self.otfv:
-                K.asw_vCostAggregation_otf_v(p, self.left, self.right, self.lut, self.c0, out=self.c1)
-            elif it == 0 and self.raw16:
+            if it == 0 and self.raw16:
                 K.asw_vCostAggregation16(p, self.wvl, self.wvr, self.c0_16, out=self.c1, den=self.den_v, den_mode=dmv)
-            elif self.vidx:
-                K.aggregate_pass_index(p, DIR_V, self.wvl, self.wvr, self.lut, self.c0, out=self.c1)
             else:
                 K.asw_vCostAggregation(p, self.wvl, self.wvr, self.c0, out=self.c1, den=self.den_v, den_mode=dmv)
             if events is not None:
                 events.append(("v", _record()))
-            if self.otf:
-                K.asw_hCostAggregation_otf(p, self.whl, self.right, self.lut, self.c1, out=self.c0, den=self.den_h,
-                                           den_mode=dm)
-            elif self.hidx:
-                K.aggregate_pass_index(p, DIR_H, self.whl, self.whr, self.lut, self.c1, out=self.c0, den=self.den_h,
-                                       den_mode=dm)
-            elif self.wta_fused and it == p.iters - 1:
-                key, m1, m2 = self._local_bufs
-                self.local = K.asw_hCostAggregation_wta_local(p, self.whl, self.whr, self.c1, self.den_h, out=self.c0,
-                                                              key=key, m1=m1, m2=m2)[1:]
-            else:
-                K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0, den=self.den_h, den_mode=dm)
+            K.asw_hCostAggregation(p, self.whl, self.whr, self.c1, out=self.c0, den=self.den_h, den_mode=dm)
             if events is not None:
                 events.append(("h", _record()))
         return self.c0
@@ -207,11 +117,10 @@ class StereoMatcher:
         p = self.p
         if events is not None:
             events.append(("start", _record()))
-        fuse = self.fuse_raw and p.iters >= 1  # asw_Aggr fused into the first V pass
-        self.raw_and_support(left, right, raw=not fuse)
+        self.raw_and_support(left, right)
         if events is not None:
             events.append(("support", _record()))
-        cost = self.aggregate(events, images=(left, right) if fuse else None)
+        cost = self.aggregate(events)
         if self.local is not None:  # the own scan ran in the last pass: the target scan and finalize
             d_ref, conf_ref, d_tar, conf_tar, code_ref, code_tar = K.wta_from_local(p, cost, *self.local)
         else:

@@ -27,7 +27,7 @@ def test_every_header_symbol_is_exported(L):
 
 def test_abi_version(L):
     import re
-    assert L.lib().asw_abi_version() == 3
+    assert L.lib().asw_abi_version() == 4
     # the binding's mirrored struct layouts are the header's revision (_load refuses others)
     hdr = open(os.path.join(ROOT, "include", "asw.h")).read()
     assert int(re.search(r"#define ASW_ABI_VERSION (\d+)", hdr).group(1)) == L.ABI_VERSION
@@ -38,7 +38,9 @@ def test_tune_set_rejects_bits_that_select_nothing(L):
     assert lib.asw_tune_set(1, 64) == L.ASW_E_INVALID      # round 1's 10-wave H form: no longer built
     assert lib.asw_tune_set(1, 1 << 28) == L.ASW_E_INVALID
     assert lib.asw_tune_set(1, 1 << 26) == 0 and lib.asw_tune_set(1, 0) == 1 << 26  # 32-plane passes: nt flipped
-    assert lib.asw_tune_set(1, 1 << 27) == 0 and lib.asw_tune_set(1, 0) == 1 << 27  # lean H form: the left ring in LDS
+    # round 6: the 32-plane H pass's 4-wave-block (bit 24) and LDS-left-ring (bit 27) forms are no longer built
+    assert lib.asw_tune_set(1, 1 << 24) == L.ASW_E_INVALID
+    assert lib.asw_tune_set(1, 1 << 27) == L.ASW_E_INVALID
     assert lib.asw_tune_set(2, 5) == L.ASW_E_INVALID
     # WTA variant 1 (wave per pixel) is no longer built (tools/exp/exp_forms.hip)
     assert lib.asw_tune_set(2, 1) == L.ASW_E_INVALID
@@ -175,40 +177,21 @@ def test_missing_library_fails_loudly(tmp_path):
     assert "LOUD" in r.stdout, (r.stdout, r.stderr[-2000:])
 
 
-def test_pass_otf_support_and_errors(L):
-    """asw_aggregate_pass_otf (on-the-fly right H weights): H, RGB, ring tap counts only;
-    the unsupported combinations fail before any launch (no GPU needed)."""
-    lib = L.lib()
-    p = L.default_params(64, 32, ndisp=16, taps=35)
-    assert lib.asw_pass_otf_supported(ctypes.byref(p), 1) == 1
-    assert lib.asw_pass_otf_supported(ctypes.byref(p), 0) == 0  # V: not built
-    q = L.default_params(64, 32, ndisp=16, taps=11)  # no ring kernel for T = 11
-    assert lib.asw_pass_otf_supported(ctypes.byref(q), 1) == 0
-    r = L.default_params(64, 32, ndisp=16, taps=35, color_space=L.COLOR_LAB)
-    assert lib.asw_pass_otf_supported(ctypes.byref(r), 1) == 0
-    x = ctypes.c_void_p(1)
-    y = ctypes.c_void_p(2)
-    for pp, d in ((p, 0), (q, 1), (r, 1)):
-        assert lib.asw_aggregate_pass_otf(ctypes.byref(pp), d, x, x, x, x, y, None, L.DEN_NONE, None) == \
-            L.ASW_E_UNSUPPORTED
-    assert lib.asw_aggregate_pass_otf(ctypes.byref(p), 1, None, x, x, x, y, None, L.DEN_NONE, None) == L.ASW_E_INVALID
-
-
 def test_params_flags(L):
-    """asw_params.flags (ABI 3): the opt-in forms are context options, not environment
-    variables; unknown bits are rejected."""
+    """asw_params.flags (ABI 4): the context options; the bits of the forms removed in
+    round 6 (measured slower in every shape) and unknown bits are rejected."""
+    import re
     p = L.default_params(32, 32)
     assert p.flags == 0
-    for f in (L.FLAG_FUSE_RAW, L.FLAG_SUPPORT_INDEX, L.FLAG_SUPPORT_INDEX_V, L.FLAG_OTF_H, L.FLAG_SHARD_DEN_H,
-              L.FLAG_COMM_LOCAL, L.FLAG_RAW_F32, L.FLAG_OTF_V, L.FLAG_WTA_FUSED):
+    for f in (L.FLAG_COMM_LOCAL, L.FLAG_RAW_F32, L.FLAG_COMM_LOCAL | L.FLAG_RAW_F32):
         p.flags = f
         assert L.params_check(p) == L.ASW_OK
-    p.flags = 0x200
-    assert L.params_check(p) == L.ASW_E_INVALID
+    for f in (0x1, 0x2, 0x4, 0x8, 0x10, 0x80, 0x100, 0x200):
+        p.flags = f
+        assert L.params_check(p) == L.ASW_E_INVALID
     hdr = open(os.path.join(ROOT, "include", "asw.h")).read()
-    for name in ("FUSE_RAW", "SUPPORT_INDEX", "SUPPORT_INDEX_V", "OTF_H", "SHARD_DEN_H", "COMM_LOCAL", "RAW_F32",
-                 "OTF_V", "WTA_FUSED"):
-        import re
+    assert sorted(re.findall(r"#define ASW_FLAG_(\w+) ", hdr)) == ["ALL", "COMM_LOCAL", "RAW_F32"]
+    for name in ("COMM_LOCAL", "RAW_F32"):
         v = int(re.search(rf"#define ASW_FLAG_{name} (0x[0-9A-Fa-f]+)", hdr).group(1), 16)
         assert v == getattr(L, f"FLAG_{name}")
     # the library reads no environment switch (the flags replaced them)
@@ -216,38 +199,18 @@ def test_params_flags(L):
     assert "getenv" not in src
 
 
-def test_pass_raw_supported(L):
-    """asw_pass_raw_supported: the fused raw-cost first V pass is built for ring tap
-    counts of this library build, not for a 32-plane shard, and needs r >= 1."""
+def test_removed_forms_are_not_exported(L):
+    """Round 6 removed the opt-in forms that lost their A/B everywhere (DESIGN.md
+    §Keep/drop): their entry points are gone from the library and the header."""
+    import re
+    hdr = open(os.path.join(ROOT, "include", "asw.h")).read()
     lib = L.lib()
-    p = L.default_params(64, 32, ndisp=64, taps=35)
-    assert lib.asw_pass_raw_supported(ctypes.byref(p)) == 1
-    assert lib.asw_pass_raw_supported(ctypes.byref(L.default_params(64, 32, ndisp=64, taps=11))) == 0
-    assert lib.asw_pass_raw_supported(ctypes.byref(L.default_params(64, 32, ndisp=64, taps=35, iters=0))) == 0
-    shard = L.default_params(64, 32, ndisp=256, taps=35, d_begin=32, d_end=64)
-    assert lib.asw_pass_raw_supported(ctypes.byref(shard)) == 0
-    from stereo_matchin_amd import kernels as K
-    assert K.raw_fused_supported(p) and not K.raw_fused_supported(shard)
-
-
-def test_pass_wta_local_supported(L):
-    """asw_pass_wta_local_supported: the local WTA scan fuses into the den-read H pass
-    where that pass is one k_hpass11 block over every plane (pitch 256 or 128, ring tap
-    counts <= 35, a frame large enough for k_hpass11)."""
-    lib = L.lib()
-    q = lambda **kw: lib.asw_pass_wta_local_supported(ctypes.byref(L.default_params(**kw)))  # noqa: E731
-    assert q(width=1920, height=1080, ndisp=256, taps=35) == 1                 # C4
-    assert q(width=1920, height=1080, ndisp=256, taps=35, d_begin=0, d_end=128) == 1  # a 2-way shard
-    assert q(width=1920, height=1080, ndisp=256, taps=51) == 0                 # T > 35
-    assert q(width=3840, height=2160, ndisp=512, taps=35) == 0                 # pitch 512
-    assert q(width=1920, height=1080, ndisp=256, taps=35, d_begin=0, d_end=32) == 0  # pitch 32
-    assert q(width=1920, height=1080, ndisp=256, taps=11) == 0                 # no ring kernel
-    assert q(width=64, height=32, ndisp=256, taps=35) == 0                     # small: k_hpass9
-    old = lib.asw_tune_set(1, 4096)  # k_hpass11 at any size
-    try:
-        assert q(width=64, height=32, ndisp=256, taps=35) == 1
-    finally:
-        lib.asw_tune_set(1, old)
+    for name in ("asw_aggregate_pass_otf", "asw_pass_otf_supported", "asw_aggregate_pass_otf_v",
+                 "asw_pass_otf_v_supported", "asw_aggregate_pass_raw", "asw_pass_raw_supported",
+                 "asw_support_all_fmt", "asw_support_index_bytes", "asw_aggregate_pass_index",
+                 "asw_pass_index_supported", "asw_aggregate_pass_wta_local", "asw_pass_wta_local_supported"):
+        assert not hasattr(lib, name), name
+        assert not re.search(rf"\b{name}\(", hdr), name
 
 
 def test_raw16_supported_and_validation(L):

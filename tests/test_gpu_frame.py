@@ -56,17 +56,13 @@ def test_multi_shard_local_equals_single(gpu, oracle, n):
     assert np.array_equal(got["d_ref"], o["d_ref"]) and np.array_equal(got["lr_red_rgba"], o["lr_red_rgba"])
 
 
-# C4's D = 256 over 8 shards of 32 planes (pitch 32: the half-wave passes), with float
-# supports (default), index-form supports (asw_params.flags ASW_FLAG_SUPPORT_INDEX /
-# ASW_FLAG_SUPPORT_INDEX_V, read at create) and the V weights on the fly (ASW_FLAG_OTF_V)
-@pytest.mark.parametrize("index", ["", "1", "v", "otfv"])
-def test_multi_shard_d256_eight_way(gpu, index):
-    from stereo_matchin_amd import FrameContext, _lib
+# C4's D = 256 over 8 shards of 32 planes (pitch 32: the half-wave passes)
+def test_multi_shard_d256_eight_way(gpu):
+    from stereo_matchin_amd import FrameContext
     Lh, Rh = _pair(7, 96, 320, shift=40)
     p = _p(320, 96, 256, 35, 2)
     with FrameContext(p, devices=[0]) as one:
         ref = one.match(Lh, Rh)
-    p.flags = {"": 0, "1": _lib.FLAG_SUPPORT_INDEX, "v": _lib.FLAG_SUPPORT_INDEX_V, "otfv": _lib.FLAG_OTF_V}[index]
     with FrameContext(p, devices=[0] * 8) as fc:
         assert [e - b for b, e in fc.shards()] == [32] * 8
         got = fc.match(Lh, Rh)
@@ -203,28 +199,6 @@ def test_graph_mode_equals_eager(gpu):
             b = graphed.match(Lh, Rh, want16=True)
             _same(b, a, KEYS + ("final_rgba", "post_red_rgba", "disp16", "lr16"))
             assert b["timings"]["total"] > 0 and b["timings"]["refine"] > 0
-
-
-# (two shards of 128 planes: each fuses its local scan; the exchange takes it from there)
-@pytest.mark.parametrize("devices", [[0], [0, 0]])
-def test_wta_fused_frame_equals_default(gpu, tune_variant, devices):
-    """ASW_FLAG_WTA_FUSED (the WTA's own scan in the last H pass, asw_aggregate_pass_wta_local)
-    through asw_match: the same maps and volume as the default frame, one shard (the
-    one-shard protocol's target scan + finalize) and several (the fused key / m1 / m2 into
-    the exchange)."""
-    from stereo_matchin_amd import FrameContext, _lib
-    tune_variant(4096)  # k_hpass11 at any size: the fused form at this test's size
-    Lh, Rh = _pair(13, 72, 300, shift=30)
-    p = _p(300, 72, 256, 35, 3)
-    with FrameContext(p, devices=devices) as fc:
-        a = fc.match(Lh, Rh, want_cost=len(devices) == 1)
-    q = p.copy()
-    q.flags = _lib.FLAG_WTA_FUSED
-    with FrameContext(q, devices=devices) as fc:
-        b = fc.match(Lh, Rh, want_cost=len(devices) == 1)
-    _same(a, b)
-    if len(devices) == 1:
-        assert np.array_equal(a["cost"], b["cost"])
 
 
 # the frame API's raw-cost forms: the uint16 volume (default where asw_raw16_supported)

@@ -198,43 +198,6 @@ def test_den_cache_write_then_read(gpu, oracle, T, direction, H, W, D, d0, d1):
         assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
 
 
-# asw_Aggr fused into the first V pass (asw_aggregate_pass_raw): bit-identical to
-# asw_raw_cost + asw_aggregate_pass_den(V), incl. a d-shard, padding planes (D not a
-# multiple of 64), truncated AD, every den mode, and the den volume it writes
-@pytest.mark.parametrize("T", [5, 9, 33, 35, 51])
-@pytest.mark.parametrize("H,W,D,d0,d1,tau", [(37, 91, 70, 0, 70, 765.0), (23, 150, 200, 70, 135, 765.0),
-                                              (40, 77, 64, 0, 64, 90.0), (3, 5, 9, 0, 9, 765.0),
-                                              (150, 70, 64, 0, 64, 765.0), (233, 37, 200, 10, 140, 90.0)])
-def test_raw_fused_first_v_pass(gpu, oracle, T, H, W, D, d0, d1, tau):
-    import torch
-
-    import stereo_matchin_amd.kernels as K
-    from stereo_matchin_amd import _lib
-    Lh, Rh = _rand_pair(T * 7 + W + D, H, W, shift=6)
-    p = _params(W, H, D, T, d_begin=d0, d_end=d1, tad_tau=tau)
-    L, R = _t(Lh, gpu), _t(Rh, gpu)
-    wl, wr = K.asw_vSupport(p, L), K.asw_vSupport(p, R)
-    c0 = K.asw_Aggr(p, L, R)
-    for mode in (_lib.DEN_NONE, _lib.DEN_WRITE):
-        den_a = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
-        den_b = den_a.clone()
-        want = K.asw_vCostAggregation(p, wl, wr, c0, den=den_a, den_mode=mode)
-        got = K.asw_vCostAggregation_raw(p, wl, wr, L, R, den=den_b, den_mode=mode)
-        # (the fused form of k_vpass10 at every ring tap count)
-        assert K.pass_kernel(0, mode).startswith(f"k_vpass10_raw<T={T},"), K.pass_kernel(0, mode)
-        n = d1 - d0
-        assert torch.equal(got[..., :n], want[..., :n]), (mode, torch.nonzero(got[..., :n] != want[..., :n])[:5])
-        if mode == _lib.DEN_WRITE:
-            assert torch.equal(den_b[..., :n], den_a[..., :n])
-    # and against the oracle's raw cost + pass
-    full = oracle.raw_cost_tad(Lh, Rh, D, tau) if tau < 765 else oracle.raw_cost(Lh, Rh, D)
-    cin = np.ascontiguousarray(full[d0:d1])
-    sl, sr = oracle.support(Lh, T, 0), oracle.support(Rh, T, 0)
-    want = oracle.aggregate_pass(sl, sr, cin, T, 0, d0=d0, d1=d1, plane_base=d0)
-    got = plane_major(_np(K.asw_vCostAggregation_raw(p, wl, wr, L, R)), d1 - d0)
-    assert np.array_equal(got, want)
-
-
 # the raw costs as uint16 (asw_raw_cost16) and the first V pass over them
 # (asw_aggregate_pass_den16, the matcher's and the frame API's default since round 5):
 # the uint16 volume holds exactly asw_raw_cost's floats, and the pass equals the float
@@ -337,8 +300,6 @@ def test_hpass_h11_bit_exact(gpu, oracle, T, H, W, D, d0, d1):
     sl, sr = oracle.support(Lh, T, 1), oracle.support(Rh, T, 1)
     wl, wr = K.asw_hSupport(p, _t(Lh, gpu)), K.asw_hSupport(p, _t(Rh, gpu))
     den = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
-    den2 = torch.full(K.cost_shape(p), float("nan"), dtype=torch.float32, device=gpu)
-    lut, R = K.support_lut(p, gpu), _t(Rh, gpu)
     old = _lib.lib().asw_tune_set(1, 4096)  # k_hpass11 below its frame-size threshold too
     try:
         for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
@@ -347,53 +308,8 @@ def test_hpass_h11_bit_exact(gpu, oracle, T, H, W, D, d0, d1):
             out = K.asw_hCostAggregation(p, wl, wr, _t(pixel_major(cin, Dp), gpu), den=den, den_mode=mode)
             got = plane_major(_np(out), d1 - d0)
             assert np.array_equal(got, want), (mode, np.argwhere(got != want)[:5])
-            # the same pass with the right weights computed on the fly
-            out = K.asw_hCostAggregation_otf(p, wl, R, lut, _t(pixel_major(cin, Dp), gpu), den=den2, den_mode=mode)
-            assert K.pass_kernel(1, mode).startswith(f"k_hpass11_otf<T={T}")
-            got = plane_major(_np(out), d1 - d0)
-            assert np.array_equal(got, want), ("otf", mode, np.argwhere(got != want)[:5])
     finally:
         _lib.lib().asw_tune_set(1, old)
-
-
-# the on-the-fly H pass through k_hpass9 (small frames) and through every compiled
-# tap count, edges included (image borders clamp the neighbour AND shorten dist)
-@pytest.mark.parametrize("T", [3, 5, 7, 9, 15, 33, 35, 51])
-@pytest.mark.parametrize("scene", ["tsukuba", "ragged"])
-def test_hpass_otf_bit_exact(gpu, oracle, T, scene):
-    import torch
-
-    import stereo_matchin_amd.kernels as K
-    from stereo_matchin_amd import _lib
-    if scene == "tsukuba":
-        Lh, Rh, _ = load_scene("tsukuba")
-        D, d0, d1 = 61, 0, 61
-    else:
-        Lh, Rh = _rand_pair(T, 37, 123)
-        D, d0, d1 = 90, 20, 90
-    H, W = Lh.shape[:2]
-    p = _params(W, H, D, T, d_begin=d0, d_end=d1)
-    Dp = K.cost_shape(p)[2]
-    assert K.otf_supported(p)
-    wl, wr = K.asw_hSupport(p, _t(Lh, gpu)), K.asw_hSupport(p, _t(Rh, gpu))
-    lut, R = K.support_lut(p, gpu), _t(Rh, gpu)
-    cin = _t(pixel_major((np.random.default_rng(T).random((d1 - d0, H, W)) * 700).astype(np.float32), Dp), gpu)
-    for variant in (0, 128, 4096):  # size-selected, k_hpass9, k_hpass11
-        old = _lib.lib().asw_tune_set(1, variant)
-        try:
-            for mode in (_lib.DEN_NONE, _lib.DEN_WRITE, _lib.DEN_READ):
-                den_a = torch.zeros(K.cost_shape(p), dtype=torch.float32, device=gpu)
-                den_b = torch.zeros(K.cost_shape(p), dtype=torch.float32, device=gpu)
-                if mode == _lib.DEN_READ:  # a real den volume to read
-                    K.asw_hCostAggregation(p, wl, wr, cin, den=den_a, den_mode=_lib.DEN_WRITE)
-                    den_b.copy_(den_a)
-                a = K.asw_hCostAggregation(p, wl, wr, cin, den=den_a, den_mode=mode)
-                b = K.asw_hCostAggregation_otf(p, wl, R, lut, cin, den=den_b, den_mode=mode)
-                assert "_otf<" in K.pass_kernel(1, mode)
-                assert torch.equal(a, b), (variant, mode)
-                assert torch.equal(den_a, den_b), (variant, mode)
-        finally:
-            _lib.lib().asw_tune_set(1, old)
 
 
 # every compiled pass variant (asw_tune_set): H block shapes (128: k_hpass9 always;
@@ -444,10 +360,10 @@ def test_wta_and_consistency_on_oracle_volume(gpu, oracle):
 
 # ------------------------------------------------------------------ end to end
 
-def _run(gpu, Lh, Rh, D, T, iters, fuse_raw=False, **kw):
+def _run(gpu, Lh, Rh, D, T, iters, **kw):
     from stereo_matchin_amd import StereoMatcher
     p = _params(Lh.shape[1], Lh.shape[0], D, T, iters, **kw)
-    m = StereoMatcher(p, gpu, fuse_raw=fuse_raw)
+    m = StereoMatcher(p, gpu)
     return p, m.match(_t(Lh, gpu), _t(Rh, gpu))
 
 
@@ -473,10 +389,11 @@ def test_e2e_tsukuba_reference_params(gpu, oracle):
     assert np.array_equal(_np(res.lr_red_rgba)[..., :3], dev_red)
 
 
-@pytest.mark.parametrize("fuse_raw", [False, True])
-def test_e2e_c1_tsukuba_d16_t5(gpu, oracle, fuse_raw):
+@pytest.mark.parametrize("raw_f32", [False, True])
+def test_e2e_c1_tsukuba_d16_t5(gpu, oracle, raw_f32):
+    from stereo_matchin_amd import _lib
     Lh, Rh, _ = load_scene("tsukuba")
-    _, res = _run(gpu, Lh, Rh, 16, 5, 7, fuse_raw=fuse_raw)
+    _, res = _run(gpu, Lh, Rh, 16, 5, 7, flags=_lib.FLAG_RAW_F32 if raw_f32 else 0)
     _compare_e2e(res, oracle.match(Lh, Rh, 16, 5, 7, want_cost=True), 16)
 
 
@@ -610,14 +527,14 @@ def test_c4_full_frame_oracle_parity(gpu, oracle):
     from stereo_matchin_amd.synthetic import make_pair
     W, H, D, T = 1920, 1080, 256, 35
     Lh, Rh, gt = make_pair(W, H, D, 0)
-    p, res = _run(gpu, Lh, Rh, D, T, 7, fuse_raw=None)  # the matcher's default (as benched)
+    p, res = _run(gpu, Lh, Rh, D, T, 7)  # the matcher's default (as benched)
     names = _pass_kernels()
     print("C4 pass kernels:", names)
     m = StereoMatcher(p, gpu)
-    fused, raw16 = m.fuse_raw, m.raw16  # the first V pass: k_vpass10_raw (fused) / k_vpass10_c16 (uint16 raw costs)
+    raw16 = m.raw16  # the first V pass: k_vpass10_c16 (uint16 raw costs)
     del m
     for dm in (1, 2):
-        v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10_c16" if raw16 and dm == 1 else "k_vpass10"
+        v = "k_vpass10_c16" if raw16 and dm == 1 else "k_vpass10"
         assert names[(0, dm)].startswith(f"{v}<T={T},NW=16,DM={dm}") and names[(0, dm)].endswith(",nt>"), names
         assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW=4,DM={dm}") and names[(1, dm)].endswith(",nt>"), \
             names
@@ -645,13 +562,13 @@ def test_c5_band_oracle_parity(gpu, oracle):
     Lh, Rh, _ = make_pair(W, H, D, 3)
     Ls, Rs = np.ascontiguousarray(Lh[900:1170]), np.ascontiguousarray(Rh[900:1170])
     del Lh, Rh
-    p, res = _run(gpu, Ls, Rs, D, T, 7, fuse_raw=None, lr_mode=1)
+    p, res = _run(gpu, Ls, Rs, D, T, 7, lr_mode=1)
     names = _pass_kernels()
     print("C5 band pass kernels:", names)
     from stereo_matchin_amd.kernels import raw16_supported
-    fused, raw16 = False, raw16_supported(p)  # the matcher's default (p.flags = 0): uint16 raw costs
+    raw16 = raw16_supported(p)  # the matcher's default (p.flags = 0): uint16 raw costs
     for dm in (1, 2):
-        v = "k_vpass10_raw" if fused and dm == 1 else "k_vpass10_c16" if raw16 and dm == 1 else "k_vpass10"
+        v = "k_vpass10_c16" if raw16 and dm == 1 else "k_vpass10"
         # 12-column blocks in 3 phases; on this 3840-wide band in XCD-round tiles of 4 plane
         # blocks (v12_tiles in asw_aggregate_impl.h)
         assert names[(0, dm)] == f"{v}<T={T},NW=12,NPH=3,TK=4,DM={dm},nt>", names

@@ -31,12 +31,13 @@ def main():
     ap.add_argument("--h", action="store_true", help="H-pass experiments")
     ap.add_argument("--vprobe", default="", help="V resource probes dm:probe,... (libexp_vprobe.so)")
     ap.add_argument("--vdma", default="", help="LDS-DMA V pass forms f,... (libexp_vdma.so)")
+    ap.add_argument("--hwta", default="", help="fused-WTA H pass variants vg,... (libexp_hwta.so)")
     args = ap.parse_args()
     W, H, D, T = (3840, 2160, 512, 51) if args.c5 else (1920, 1080, 256, 35)
     dev = torch.device("cuda:0")
     Lh, Rh, _ = make_pair(W, H, D, 0)
     p = make_params(W, H, ndisp=D, taps=T, iters=7, flags=_lib.FLAG_RAW_F32)  # c0 = the float raw costs
-    m = StereoMatcher(p, dev, otf=False)
+    m = StereoMatcher(p, dev)
     m.raw_and_support(torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev))
     # a realistic H input: one V pass of the raw cost
     cin = torch.empty_like(m.c0)
@@ -99,6 +100,63 @@ def main():
                     res.setdefault(name, []).append(e0.elapsed_time(e1))
         for name, ts in res.items():
             print(json.dumps({"exp": name, "ms_median": round(float(np.median(ts)), 4)}), flush=True)
+        return
+    if args.hwta:
+        # the last H pass with the WTA's own scan fused (asw_hwta.h) against the production
+        # den-read H pass + asw_wta_local, bit-exact (volume, key, m1, m2); then the frame's
+        # WTA tail both ways: asw_WTA (k_wta_scan: own + target scan) against the fused
+        # pass's scan + asw_wta_target_local + asw_wta_finalize
+        lx = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp_hwta.so"))
+        key_r, m1_r, m2_r = K.wta_local(p, ref)
+        Hh, Wh = p.height, p.width
+        key = torch.empty((Hh, Wh), dtype=torch.int64, device=dev)
+        m1 = torch.empty((Hh, Wh), dtype=torch.float32, device=dev)
+        m2 = torch.empty((Hh, Wh), dtype=torch.float32, device=dev)
+        wta_ref = K.asw_WTA(p, ref)
+        torch.cuda.synchronize()
+        vgs = [int(v) for v in args.hwta.split(",")]
+        res = {}
+        cur = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
+        for rep in range(args.reps + 1):
+            cases = [("h_read_prod", None)] + [(f"h_read_wta_vg{v}", v) for v in vgs]
+            for name, vg in cases:
+                out.zero_()
+                key.zero_()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                if vg is None:
+                    K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=out, den=den, den_mode=2)
+                else:
+                    rc = lx.exp_hwta(vg, pp, P(m.whl), P(m.whr), P(cin), P(out), P(den), P(key), P(m1), P(m2), cur())
+                    assert rc == 0, (name, rc)
+                e1.record()
+                torch.cuda.synchronize()
+                if rep == 0:
+                    ok = bool(torch.equal(out, ref))
+                    if vg is not None:
+                        ok = ok and bool(torch.equal(key, key_r)) and bool(torch.equal(m1, m1_r)) and \
+                            bool(torch.equal(m2, m2_r))
+                        got = K.wta_from_local(p, out, key, m1, m2)
+                        ok = ok and all(bool(torch.equal(a_, b_)) for a_, b_ in zip(got, wta_ref))
+                    print(json.dumps({"exp": name, "bit_exact": ok}), flush=True)
+                else:
+                    res.setdefault(name, []).append(e0.elapsed_time(e1))
+            # the WTA tails on the same volume
+            for name in ("wta_scan", "wta_target_finalize"):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                if name == "wta_scan":
+                    K.asw_WTA(p, ref)
+                else:
+                    K.wta_from_local(p, ref, key_r, m1_r, m2_r)
+                e1.record()
+                torch.cuda.synchronize()
+                if rep:
+                    res.setdefault(name, []).append(e0.elapsed_time(e1))
+        for name, ts in res.items():
+            print(json.dumps({"exp": name, "ms_median": round(float(np.median(ts)), 4), "ms_min": round(min(ts), 4)}),
+                  flush=True)
         return
     if args.vdma:
         # the LDS-DMA-staged V pass (asw_vdma.h) against the production pass, every den mode:

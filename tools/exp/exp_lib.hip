@@ -168,10 +168,10 @@ extern "C" int exp_h32(int form, int nseg, int dm, const asw_params *p, const fl
     if (nseg <= 0) nseg = (slots + pairs / 2) / (pairs > 0 ? pairs : 1);
     int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
     if (seg < 2 * U) seg = 2 * U;
-    if (form == 0) launch_h32<T, 1, DM_NONE, 0, 4, true, 3, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
-    else if (form == 1) launch_h32<T, 1, DM_NONE, 0, 4, false, 3, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
-    else if (form == 2) launch_h32<T, 1, DM_NONE, 0, 4, false, 4, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
-    else if (form == 3) launch_h32<T, 1, DM_NONE, 0, 4, true, 4, false, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    if (form == 0) launch_h32<T, 1, DM_NONE, 0, 4, true, 3, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    else if (form == 1) launch_h32<T, 1, DM_NONE, 0, 4, false, 3, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    else if (form == 2) launch_h32<T, 1, DM_NONE, 0, 4, false, 4, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    else if (form == 3) launch_h32<T, 1, DM_NONE, 0, 4, true, 4, 0, true>(p, wl, wr, cin, cout, den, st, seg);
     else return -4;
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -238,5 +238,23 @@ extern "C" int exp_vdma(int form, int dm, const asw_params *p, const float *wl, 
     VD(64, 6, 8)
 #undef VD
     return -4;
+}
+#endif
+
+#ifdef EXP_HWTA
+// the last H pass with the WTA's own scan fused by DPP reductions (round 6, asw_hwta.h)
+#include "asw_hwta.h"
+extern "C" int exp_hwta(int vg, const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                        float *den, long long *key, float *m1, float *m2, void *stream) {
+    if (p->taps != 35) return -4;
+    const int Dp = asw_disp_pitch(p);
+    constexpr int U = pf9_period(35);
+    const int seg = ((240 + U / 2) / U) * U;
+    hipStream_t st = (hipStream_t)stream;
+    if (Dp == 256 && vg == 0) launch_h11_wr<35, 4, 0>(p, wl, wr, cin, cout, den, key, m1, m2, st, seg);
+    else if (Dp == 256 && vg == 1) launch_h11_wr<35, 4, 1>(p, wl, wr, cin, cout, den, key, m1, m2, st, seg);
+    else if (Dp == 128 && vg == 0) launch_h11_wr<35, 2, 0>(p, wl, wr, cin, cout, den, key, m1, m2, st, seg);
+    else return -4;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif

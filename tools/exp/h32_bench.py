@@ -31,7 +31,7 @@ def main():
     Lh, Rh, _ = make_pair(W, H, D, 0)
     p = make_params(W, H, ndisp=D, taps=T, iters=7, flags=_lib.FLAG_RAW_F32)
     p.d_begin, p.d_end = 0, 32
-    m = StereoMatcher(p, dev, otf=False, support_index=False)
+    m = StereoMatcher(p, dev)
     m.raw_and_support(torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev))
     cin = torch.empty_like(m.c0)
     K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=cin)  # a realistic H input

@@ -45,61 +45,39 @@ def main():
     p = make_params(W, H, ndisp=D, taps=T, iters=iters, flags=_lib.FLAG_RAW_F32)  # c0 = the float raw costs
     if args.planes:
         p.d_begin, p.d_end = 0, args.planes
-    # float supports (materialised whr too: both H forms are timed); a 32-plane shard's V
-    # pass over index-form supports (asw_aggregate_pass_index) is timed as "v_idx"
-    m = StereoMatcher(p, dev, otf=False, support_index=False)
+    m = StereoMatcher(p, dev)
     Ld, Rd = torch.from_numpy(Lh).to(dev), torch.from_numpy(Rh).to(dev)
     m.raw_and_support(Ld, Rd)
-    vidx = K.index_supported(p, 0, 0)
-    if vidx:
-        ivl, ivr, ihl, ihr = (K.new_support_index(p, dev) for _ in range(4))
-        K.support_all(p, Ld, Rd, m.lut, ivl, ihl, ivr, ihr)
     torch.cuda.synchronize()
     cin = m.c0
     out = torch.empty_like(cin)
     variants = [int(v) for v in args.variants.split(",")]
     modes = [0, 1, 2] if args.den else [0]  # ASW_DEN_NONE / WRITE / READ
-    dens = {"v": torch.empty_like(cin), "h": torch.empty_like(cin), "h_otf": torch.empty_like(cin),
-            "h_idx": torch.empty_like(cin)} if args.den else {}
+    dens = {"v": torch.empty_like(cin), "h": torch.empty_like(cin)} if args.den else {}
     lib = _lib.lib()
     S = W * H
     nloc = p.d_stop - p.d_begin
     nbytes = 8 * nloc * S + 8 * T * S
-    dirs = ("v", "h", "h_otf") if K.otf_supported(p) else ("v", "h")
-    if vidx:
-        dirs = dirs + ("v_idx", "h_idx")
+    dirs = ("v", "h")
     ref = {}
     kname = {}
-    times = {(v, d, dm): [] for v in variants for d in dirs for dm in modes if d != "v_idx" or dm == 0}
+    times = {(v, d, dm): [] for v in variants for d in dirs for dm in modes}
     for rep in range(args.reps + 1):
         for v in variants:
             lib.asw_tune_set(1, v)
-            right = torch.from_numpy(Rh).to(dev)
-            otf = lambda p_, wl_, wr_, cin_, out=None, den=None, den_mode=0: K.asw_hCostAggregation_otf(  # noqa: E731
-                p_, wl_, right, m.lut, cin_, out=out, den=den, den_mode=den_mode)
-            vix = lambda p_, wl_, wr_, cin_, out=None, den=None, den_mode=0: K.aggregate_pass_index(  # noqa: E731
-                p_, 0, wl_, wr_, m.lut, cin_, out=out)
-            hix = lambda p_, wl_, wr_, cin_, out=None, den=None, den_mode=0: K.aggregate_pass_index(  # noqa: E731
-                p_, 1, wl_, wr_, m.lut, cin_, out=out, den=den, den_mode=den_mode)
             forms = [("v", K.asw_vCostAggregation, m.wvl, m.wvr), ("h", K.asw_hCostAggregation, m.whl, m.whr)]
-            if "h_otf" in dirs:
-                forms.append(("h_otf", otf, m.whl, None))
-            if vidx:
-                forms.append(("v_idx", vix, ivl, ivr))
-                forms.append(("h_idx", hix, ihl, ihr))
             for d, fn, wl, wr in forms:
-                for dm in (modes if d != "v_idx" else [0]):
+                for dm in modes:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     fn(p, wl, wr, cin, out=out, den=dens.get(d), den_mode=dm)
                     e1.record()
                     torch.cuda.synchronize()
                     if rep == 0:
-                        kname[(d, dm)] = K.pass_kernel(0 if d in ("v", "v_idx") else 1, dm)
-                        key = {"h_otf": "h", "v_idx": "v", "h_idx": "h"}.get(d, d)
-                        if v == variants[0] and dm == 0 and d in ("v", "h"):
+                        kname[(d, dm)] = K.pass_kernel(0 if d == "v" else 1, dm)
+                        if v == variants[0] and dm == 0:
                             ref[d] = out.clone()
-                        elif not torch.equal(out, ref[key]):
+                        elif not torch.equal(out, ref[d]):
                             print(json.dumps({"variant": v, "dir": d, "den_mode": dm,
                                               "error": "output differs from variant 0"}))
                     else:

@@ -28,8 +28,6 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--workload", default="c4", choices=["c4", "c5"],
                     help="c4: 1920x1080 D256 T35; c5: 3840x2160 D512 T51 (native LR)")
-    ap.add_argument("--support-index", default="", choices=["", "1", "v"],
-                    help="index-form supports (asw_aggregate_pass_index): both directions, or V only (A/B)")
     ap.add_argument("--variants", default="0")
     ap.add_argument("--pipeline", default="",
                     help="also time the frames streamed through distributed.PipelinedMatcher (2 sets of volumes, "
@@ -48,8 +46,7 @@ def main():
     ms_ = {}
     for f in [int(x) for x in a.flags.split(",")]:
         p = make_params(W, H, ndisp=D, taps=T, iters=r, lr_check=1, lr_mode=1 if D > 256 else 0, flags=f)
-        ms_[f] = ShardedStereoMatcher(p, a.rank, a.world, dev,
-                                      support_index={"": None, "1": True, "v": "v"}[a.support_index])
+        ms_[f] = ShardedStereoMatcher(p, a.rank, a.world, dev)
     for _ in range(a.rounds):
         for v, f in [(int(x), f) for x in a.variants.split(",") for f in ms_]:
             m = ms_[f]
@@ -64,8 +61,7 @@ def main():
             lib.asw_tune_set(1, old)
             print(json.dumps({"workload": a.workload, "world": a.world, "rank": a.rank,
                               "planes": m.p.d_stop - m.p.d_begin, "variant": v, "flags": f,
-                              "raw16": m.matcher.raw16, "otf_v": m.matcher.otfv,
-                              "support_index": {"v": m.matcher.vidx, "h": m.matcher.hidx},
+                              "raw16": m.matcher.raw16,
                               "ms_per_shard_frame_no_collective": round(ms, 3)}), flush=True)
     # streamed frames (what bench.py --gpus N runs per rank), per overlap_prep value
     for ov in [int(x) for x in a.pipeline.split(",") if x != ""]:
