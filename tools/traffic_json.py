@@ -28,24 +28,28 @@ def key_of(name: str):
     """k_vpass10<35, 16, 2, ...> -> k_vpass10<T=35,DM_READ>; k_hpass9<35, 4, 40, 2> ->
     k_hpass9<T=35,DM_READ>; k_hpass11<35, 4, 2, ...> -> k_hpass11<T=35,DM_READ> (template
     argument order of each kernel; bench.py looks the kernel asw_pass_kernel names up this way)."""
-    m = re.match(r"(k_vpass10|k_vpass9|k_hpass9|k_hpass11|k_vpass32|k_hpass32)<([^>]*)>", name)
+    m = re.match(r"(k_vpass10|k_hpass9|k_hpass11_wr|k_hpass11|k_vpass32|k_hpass32)<([^>]*)>", name)
     if not m:
         return None
     args = [a.strip() for a in m.group(2).split(",")]
+    if m.group(1) == "k_hpass11_wr":  # the last H pass with the WTA's own scan (den-read)
+        return f"k_hpass11_wr<T={args[0]},DM_READ>"
     dm = int(args[3]) if m.group(1) == "k_hpass9" else int(args[2])
-    otf = m.group(1) == "k_hpass11" and len(args) > 5 and args[5] == "true"  # right weights on the fly
-    return f"{m.group(1)}{'_otf' if otf else ''}<T={args[0]},{DM[dm]}>"
+    # the first V pass over the uint16 raw costs: k_vpass10<..., C16 = true> (the last argument)
+    c16 = m.group(1) in ("k_vpass10", "k_vpass32") and args[-1] == "true"
+    return f"{m.group(1)}{'_c16' if c16 else ''}<T={args[0]},{DM[dm]}>"
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--key", default="c4_n1")
+    ap.add_argument("--source", default="", help="the tracked copy of root under profiles/ (recorded as the source)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "traffic.json"))
     a = ap.parse_args()
     raw = collect(a.root)
-    entry = {"source": a.root,
+    entry = {"source": a.source or a.root,
              "corrections": "hbm_read = 2 x FETCH_SIZE x 1024, hbm_write = WRITE_SIZE x 1024 "
                             "(calibrated: profiles/r02/calib.json)"}
     for name, c in raw.items():
