@@ -10,6 +10,11 @@
 //              16: 4 taps per half computed (VALU cut to ~1/4)
 //              32: no barrier in the sweep (LDS races)
 //              64: den loads from the chunk's first row (den-read)
+//             128: NOT a probe, bit-exact: waves 8-15 cross each barrier half a step later
+//                  in their step than waves 0-7 (after their half-A taps), so the two
+//                  groups run half a step apart and one group's LDS requests and waits
+//                  overlap the other's taps; NBUF = 8 (a put then overwrites a row whose
+//                  last readers passed an earlier barrier of both groups)
 #pragma once
 #include "asw_aggregate_impl.h"
 
@@ -23,7 +28,7 @@ __global__ __launch_bounds__(16 * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     int xg_per_xcd) {
     constexpr int NW = 16, RB = 2, CP = kCPStream, CPS = kCPStream;
     constexpr bool PC = PROBE & 1, PO = PROBE & 2, PSL = PROBE & 4, PWL = PROBE & 8, PV = PROBE & 16,
-                   PNB = PROBE & 32, PD = PROBE & 64;
+                   PNB = PROBE & 32, PD = PROBE & 64, STAG = PROBE & 128;
     constexpr int R = T / 2;
     constexpr int TP = tap_pitch(T);
     constexpr int Q = TP / 4;
@@ -31,7 +36,7 @@ __global__ __launch_bounds__(16 * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     constexpr int P = U - T;
     constexpr int PS = 4, PW = 4, KD = 2;
     constexpr int LEAD = RB + 1;
-    constexpr int NBUF = ring_div(U, 2 * RB + 1);
+    constexpr int NBUF = STAG ? ring_div(U, 3 * RB + 2) : ring_div(U, 2 * RB + 1);
     constexpr int LA = cmax(cmax(R + P, LEAD + PS), cmax(PW, KD));
     constexpr int SLAB = NW + 63;
     constexpr int NQ = SLAB * Q;
@@ -51,6 +56,7 @@ __global__ __launch_bounds__(16 * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int y_end = min(H, y_begin + rows_per_strip);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool late = STAG && wave >= NW / 2;  // (uniform) the group that crosses barriers mid-step
     const int kb = kbi * 64;
     const int x = min(x0 + wave, W - 1);
     const int slab_base = x0 - (d_begin + kb) - 63;
@@ -125,8 +131,12 @@ __global__ __launch_bounds__(16 * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
             }
             constexpr int bcur = s % NBUF, bnext = (s + 1) % NBUF, bput = (s + LEAD) % NBUF;
             float num = 1e-5f, dn = 1e-5f;
-            if constexpr (s % RB == 0 && !PNB) __syncthreads();
-            else wait_lgkm0();
+            if constexpr (s % RB == 0 && !PNB) {
+                if (late) wait_lgkm0();
+                else __syncthreads();
+            } else {
+                wait_lgkm0();
+            }
             asm volatile("" ::"v"(win[(s + T - 1) % U]));
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (HV::TB > 0) {
@@ -139,6 +149,9 @@ __global__ __launch_bounds__(16 * 64) __attribute__((amdgpu_waves_per_eu(4))) vo
             taps<U, s, 0, TAE, DM != DM_READ>(num, dn, wla, wra, win);
             __builtin_amdgcn_sched_barrier(0);
             wait_lgkm0();
+            if constexpr (STAG && s % RB == 0) {
+                if (late) __syncthreads();
+            }
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (!PWL) {
                 if constexpr (CLAMP) {

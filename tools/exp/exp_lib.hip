@@ -190,8 +190,9 @@ extern "C" int exp_vprobe(int probe, int dm, const asw_params *p, const float *w
         launch_vprobe<35, DMV, PR>(p, wl, wr, cin, cout, den, st);                                                  \
         return hipGetLastError() == hipSuccess ? 0 : -2;                                                             \
     }
-    VP(0, 0) VP(0, 3) VP(0, 15) VP(0, 16) VP(0, 32) VP(0, 47) VP(0, 19) VP(0, 8)
-    VP(2, 0) VP(2, 67) VP(2, 16) VP(2, 32)
+    VP(0, 0) VP(0, 8)
+    VP(2, 0) VP(2, 4) VP(2, 8) VP(2, 79)
+    VP(0, 128) VP(1, 128) VP(2, 128)
 #undef VP
     return -4;
 }
