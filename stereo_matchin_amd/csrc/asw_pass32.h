@@ -34,6 +34,26 @@ namespace agg {
 
 constexpr int kPlanes32 = 32;
 
+// Half-size tap-major supports (odd T, R = T/2).  The weight is symmetric in its pixel
+// pair (K/asw_vsupport.cl:19-25, K/asw_hsupport.cl:19-26: |p - q| per channel and the
+// distance), so w(p, tap R - u) is the weight of the pixel u steps back at tap R + u,
+// and at the clamped border (p - u before the first pixel: the neighbour clamps to
+// pixel 0 at distance p) that of pixel 0 at tap R + p.  An array holds taps R..2R only,
+// as [line][u][pos] (u = tap - R; line = row for V / column... the pass axis is pos for
+// H); element index of tap t of the entry at (line, pos) along the pass axis `a`:
+//   V: line = y (pass axis), pos = x;   t >= R: (y, t-R, x);  t < R, u = R-t:
+//      (y-u, u, x) if y >= u, else (0, y, x).
+// hs_index<T>(a, t, c, W): V form (a = row, c = column); taps >= T are padding (never
+// read by the taps, the load is kept in range).
+template <int T>
+__device__ __forceinline__ int hs_index(int a, int t, int c, int W) {
+    constexpr int R = T / 2, RH = R + 1;
+    if (t >= T) t = R;  // padding: any in-range element
+    if (t >= R) return (a * RH + (t - R)) * W + c;
+    const int u = R - t;
+    return a >= u ? ((a - u) * RH + u) * W + c : a * W + c;
+}
+
 // taps [B, E) of a phase with per-lane left weights (wl, wr hold taps from B)
 template <int U, int S, int B, int E, bool DEN, int M>
 __device__ __forceinline__ void taps32(float &num, float &den, const f4 (&wl)[M], const f4 (&wr)[M],
@@ -73,7 +93,10 @@ __device__ __forceinline__ void taps32_dl(float &num, float &den, const f4 &wl, 
 // weights in NPH phases with two phases' sets live).
 // ---------------------------------------------------------------------------
 // C16: the first V pass over the uint16 raw costs (asw_raw_cost16), as k_vpass10<C16>.
-template <int T, int NW, int DM, int CP, int NPH, int RB = 2, int PS = 4, bool C16 = false>
+// HS: wl / wr are half-size tap-major supports (hs_index below): each staged float4 of
+// an entry is assembled from 4 dwords, the slab in LDS is the same as from the full
+// arrays, so the taps and the outputs are unchanged.
+template <int T, int NW, int DM, int CP, int NPH, int RB = 2, int PS = 4, bool C16 = false, bool HS = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 4 : 2))) void k_vpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
     float *__restrict__ den, int W, int H, int d_begin, int rows_per_strip, int nxb, int nstrip, int xg_per_xcd) {
@@ -150,13 +173,51 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     const bool r0 = t0 / Q < NER, r1 = t1 / Q < NER;
     const float *src0 = (r0 ? wr : wl) + o0;
     const float *src1 = (r1 ? wr : wl) + o1;
+    // HS: threads [0, NSR) stage the right entries, [NSR, NSR + NER... ) the left ones
+    // (wave-uniform array: one buffer resource per wave), q-major inside each part so the
+    // lanes of a dword load are consecutive columns of one tap row (coalesced), and the
+    // b128 slab write of consecutive entries keeps its odd-Q stride (conflict-free)
+    constexpr int NSR = (NER * Q + 63) / 64 * 64;
+    static_assert(!HS || (NSR + NC * Q <= NW * 64 && NSTAGE == 1), "HS: one share per thread");
+    const int th = (int)threadIdx.x;
+    const bool hs_right = th < NSR;
+    const int hs_n = hs_right ? NER : NC;
+    const int hs_t = hs_right ? min(th, NER * Q - 1) : min(th - NSR, NC * Q - 1);
+    const int hs_e = hs_t % hs_n, hs_q = hs_t / hs_n;
+    const int hs_col = hs_right ? clampi(x0 - d_begin - 31 + hs_e, 0, W - 1) : min(x0 + hs_e, W - 1);
+    const int hs_slot = ((hs_right ? 0 : NER) + hs_e) * Q + hs_q;
+    const rsrc_t hs_rs = make_rsrc(__builtin_amdgcn_readfirstlane((int)hs_right) ? wr : wl);
+    // rows >= R (all but the first R of the image): element offset of tap 4q+j = (row -
+    // R) * (R+1) * W (scalar) + hs_off[j], its offset at row R (the vector offset stays
+    // non-negative: the buffer range check takes it as unsigned)
+    int hs_off[HS ? 4 : 1];
+    if constexpr (HS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hs_off[j] = hs_index<T>(R, 4 * hs_q + j, hs_col, W);
+    }
     auto stage = [&](f4 &a, f4 &b, int row) __attribute__((always_inline)) {
-        a = *reinterpret_cast<const f4 *>(src0 + row * wrow);
-        if constexpr (NSTAGE > 1) b = *reinterpret_cast<const f4 *>(src1 + row * wrow);
+        if constexpr (HS) {
+            if (row >= R) {
+                const int so = (row - R) * (R + 1) * W * 4;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a[j] = bload(hs_rs, hs_off[j] * 4, so);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    a[j] = bload(hs_rs, hs_index<T>(row, 4 * hs_q + j, hs_col, W) * 4, 0);
+            }
+        } else {
+            a = *reinterpret_cast<const f4 *>(src0 + row * wrow);
+            if constexpr (NSTAGE > 1) b = *reinterpret_cast<const f4 *>(src1 + row * wrow);
+        }
     };
     auto put = [&](int buf, const f4 &a, const f4 &b) __attribute__((always_inline)) {
-        slab[buf][t0] = a;
-        if constexpr (NSTAGE > 1) slab[buf][t1] = b;
+        if constexpr (HS) {
+            slab[buf][hs_slot] = a;
+        } else {
+            slab[buf][t0] = a;
+            if constexpr (NSTAGE > 1) slab[buf][t1] = b;
+        }
     };
 
     using PH = Phases<T, NPH>;
@@ -489,7 +550,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 // ---------------------------------------------------------------------------
 // launchers (one (T, DM) per translation unit: build/p32_t<T>_d<DM>.hip)
 // ---------------------------------------------------------------------------
-template <int T, int NW, int DM, int CP, int NPH, bool C16 = false>
+template <int T, int NW, int DM, int CP, int NPH, bool C16 = false, bool HS = false>
 void launch_v32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
                 hipStream_t st) {
     constexpr int U = pf9_period(T);
@@ -508,7 +569,7 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
     const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
     nstrip = (H + rows - 1) / rows;
     const int per_xcd = (nxb + 7) / 8;
-    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, 2, 4, C16>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl,
+    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, 2, 4, C16, HS>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl,
                        wr, cin, cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd);
     note_pass_kernel(ASW_DIR_V, DM, C16 ? "k_vpass32_c16" : "k_vpass32", T,
                      NW == 16 ? (NPH == 4 ? "NW=16,NPH=4" : "NW=16") : "NW=8,NPH=3", CP == kCPStream);

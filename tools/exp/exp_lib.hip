@@ -259,3 +259,39 @@ extern "C" int exp_hwta(int vg, const asw_params *p, const float *wl, const floa
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
+
+#ifdef EXP_HS
+// Half-size tap-major supports on the 32-plane shard V pass:
+// exp_hs_convert writes the [H][R+1][W] half of a full [H][W][Tp] V support array,
+// exp_hs_expand rebuilds a full array from a half one through hs_index (the symmetry
+// and border rule, checked element for element by tools/exp/hs_bench.py), exp_v32hs
+// runs k_vpass32 on the full (hs 0) or half (hs 1) arrays.
+#include "asw_pass32.h"
+__global__ void k_hs_convert(const float *__restrict__ full, float *__restrict__ half, int W, int H) {
+    constexpr int T = 35, R = T / 2, TP = asw::tap_pitch(T);
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, u = blockIdx.z;
+    if (x >= W) return;
+    half[((long long)y * (R + 1) + u) * W + x] = full[((long long)y * W + x) * TP + R + u];
+}
+__global__ void k_hs_expand(const float *__restrict__ half, float *__restrict__ full, int W, int H) {
+    constexpr int T = 35, TP = asw::tap_pitch(T);
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, t = blockIdx.z;
+    if (x >= W) return;
+    full[((long long)y * W + x) * TP + t] = t < T ? half[hs_index<T>(y, t, x, W)] : 0.0f;
+}
+extern "C" int exp_hs_convert(int expand, const float *src, float *dst, int W, int H, void *stream) {
+    constexpr int T = 35, R = T / 2;
+    const dim3 grid((W + 255) / 256, H, expand ? asw::tap_pitch(T) : R + 1);
+    if (expand) hipLaunchKernelGGL(k_hs_expand, grid, dim3(256), 0, (hipStream_t)stream, src, dst, W, H);
+    else hipLaunchKernelGGL(k_hs_convert, grid, dim3(256), 0, (hipStream_t)stream, src, dst, W, H);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+extern "C" int exp_v32hs(int hs, const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                         void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (p->taps != 35) return -4;
+    if (hs) launch_v32<35, 16, DM_NONE, 0, 4, false, true>(p, wl, wr, cin, cout, nullptr, st);
+    else launch_v32<35, 16, DM_NONE, 0, 4, false, false>(p, wl, wr, cin, cout, nullptr, st);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+#endif
