@@ -42,9 +42,13 @@ extern "C" int exp_c5(int dir, int shape, int dm, const asw_params *p, const flo
                       const float *cin, float *cout, float *den, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     if (p->taps != 51 || dm != 2 || dir != 0) return -4;
+#ifndef C5_TK
+#define C5_TK 0
+#endif
+    // (C5_TK: the XCD-round tile order of the shipped C5 V pass, round 6)
     if (shape == C5_NW * 100 + C5_NPH * 10 + C5_RB)
-        launch_v10<51, C5_NW, DM_READ, C5_RB, kCPStream, kCPStream, C5_RB == 1 ? 2 : 4, C5_NPH>(p, wl, wr, cin, cout,
-                                                                                               den, st);
+        launch_v10<51, C5_NW, DM_READ, C5_RB, kCPStream, kCPStream, C5_RB == 1 ? 2 : 4, C5_NPH, false, C5_TK>(
+            p, wl, wr, cin, cout, den, st);
     else
         return -4;
     return hipGetLastError() == hipSuccess ? 0 : -2;
