@@ -35,8 +35,12 @@ def key_of(name: str):
     if m.group(1) == "k_hpass11_wr":  # the last H pass with the WTA's own scan (den-read)
         return f"k_hpass11_wr<T={args[0]},DM_READ>"
     dm = int(args[3]) if m.group(1) == "k_hpass9" else int(args[2])
-    # the first V pass over the uint16 raw costs: k_vpass10<..., C16 = true> (the last argument)
-    c16 = m.group(1) in ("k_vpass10", "k_vpass32") and args[-1] == "true"
+    # the first V pass over the uint16 raw costs: k_vpass10<..., C16 = true> (its last
+    # argument), k_vpass32<T, NW, DM, CP, NPH, RB, PS, C16[, HS]> (the eighth)
+    if m.group(1) == "k_vpass32":
+        c16 = len(args) > 7 and args[7] == "true"
+    else:
+        c16 = m.group(1) == "k_vpass10" and args[-1] == "true"
     return f"{m.group(1)}{'_c16' if c16 else ''}<T={args[0]},{DM[dm]}>"
 
 
