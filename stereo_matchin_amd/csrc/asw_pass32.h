@@ -339,14 +339,16 @@ constexpr int h32_batch(int T) { return tap_pitch(T) / 4 * 8 <= 64 * 4 ? 4 : 2; 
 // (Round 5: the weights requested two phases ahead instead of one measured 0.3115
 // against 0.3173 ms per pass and the same shard frame, profiles/r05/pd2_nt_r12c.log;
 // not kept.)
-template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, int KB = 0, bool DL = false>
+// PX: extra cost-prefetch steps (tools/exp; the left-weight ring then keeps a 5-step lead)
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, int KB = 0, bool DL = false,
+          int PX = 0>
 __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_hpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
     float *__restrict__ den, int W, int H, int d_begin, int nseg, int seg_len, int npairs, int pairs_per_xcd) {
     constexpr int R = T / 2;
     constexpr int TP = tap_pitch(T);
     constexpr int Q = TP / 4;
-    constexpr int U = pf9_period(T);
+    constexpr int U = pf9_period(T) + PX;
     constexpr int P = U - T;
     constexpr int KD = 4;  // den prefetch ring (steps)
     constexpr int K = KB ? KB : h32_batch(T);
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
     using gf4 = const __attribute__((address_space(1))) f4;
     gelem_t *wlsrc = (gelem_t *)(wle + (long long)y * W * TP + 4 * min(lane & 15, Q - 1));
     auto wl_load = [&](int x) __attribute__((always_inline)) { return *(gf4 *)(wlsrc + min(x, W - 1) * TP); };
-    constexpr int NLD = DL ? ring_div(U, P) : 1;  // left columns in flight (>= the window's P)
+    constexpr int NLD = DL ? ring_div(U, PX ? 5 : P) : 1;  // left columns in flight (>= the window's P)
     f4 wld[NLD];
     if constexpr (DL) {
 #pragma unroll
@@ -575,7 +577,8 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
                      NW == 16 ? (NPH == 4 ? "NW=16,NPH=4" : "NW=16") : "NW=8,NPH=3", CP == kCPStream);
 }
 
-template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, int KB = 0, bool DL = false>
+template <int T, int NWB, int DM, int CP, int NPH, bool RING16 = true, int WPE = 2, int KB = 0, bool DL = false,
+          int PX = 0>
 void launch_h32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
                 hipStream_t st, int seg_len) {
     const int W = p->width, H = p->height;
@@ -583,9 +586,10 @@ void launch_h32(const asw_params *p, const float *wl, const float *wr, const flo
     const int npairs = (H + 1) / 2 * nseg;  // work items: (row pair, segment)
     const int per_xcd = (npairs + 7) / 8;
     const int blocks_per_xcd = (per_xcd + NWB - 1) / NWB;
-    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE, KB, DL>), dim3(8 * blocks_per_xcd), dim3(NWB * 64),
+    hipLaunchKernelGGL((k_hpass32<T, NWB, DM, CP, NPH, RING16, WPE, KB, DL, PX>), dim3(8 * blocks_per_xcd), dim3(NWB * 64),
                        0, st, wl, wr, cin, cout, den, W, H, p->d_begin, nseg, seg_len, npairs, per_xcd);
-    note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T, DL ? "NWB=1,NPH=4,DL" : NWB == 4 ? "NWB=4" : "NWB=2",
+    note_pass_kernel(ASW_DIR_H, DM, "k_hpass32", T,
+                     DL ? (PX ? "NWB=1,NPH=4,DL,PX=8" : "NWB=1,NPH=4,DL") : NWB == 4 ? "NWB=4" : "NWB=2",
                      CP == kCPStream);
 }
 
@@ -633,11 +637,19 @@ int launch_pass32_tm(const asw_params *p, int dir, const float *wl, const float 
         int nseg = (slots + pairs / 2) / (pairs > 0 ? pairs : 1);
         if ((g_pass_variant >> 20) & 15) nseg = (g_pass_variant >> 20) & 15;
         if (nseg < 1) nseg = 1;
-        int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
-        if (seg < 2 * U) seg = 2 * U;
+        // (T = 35: the window period of the deeper-prefetch form below)
+        constexpr int UH = T == 35 ? pf9_period(T) + 8 : U;
+        int seg = ((p->width + nseg - 1) / nseg + UH - 1) / UH * UH;
+        if (seg < 2 * UH) seg = 2 * UH;
         if constexpr (T <= 35) {
-            if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3, 0, true>(p, wl, wr, cin, cout, den, st, seg);
-            else launch_h32<T, 1, DM, 0, 4, true, 3, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+            // T = 35 (the C4 shard): the newest window element requested 13 instead of 5
+            // steps ahead (the pass waits on vmcnt, not LDS: SQ_WAIT_INST_ANY 0.34 of its
+            // wave cycles, WAIT_INST_LDS 0.006, profiles/r06/pmc_shard8_r15d.json), and
+            // 48-column window periods tile the C4 segments of 384 columns exactly:
+            // 0.286 against 0.295 ms per pass (profiles/r06/h32_px_r15f.log)
+            constexpr int PXH = UH - U;
+            if (stream) launch_h32<T, 1, DM, kCPStream, 4, true, 3, 0, true, PXH>(p, wl, wr, cin, cout, den, st, seg);
+            else launch_h32<T, 1, DM, 0, 4, true, 3, 0, true, PXH>(p, wl, wr, cin, cout, den, st, seg);
         } else {
             if (stream) launch_h32<T, 2, DM, kCPStream, 2>(p, wl, wr, cin, cout, den, st, seg);
             else launch_h32<T, 2, DM, 0, 2>(p, wl, wr, cin, cout, den, st, seg);

@@ -166,9 +166,10 @@ extern "C" int exp_h32(int form, int nseg, int dm, const asw_params *p, const fl
                        const float *cin, float *cout, float *den, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     if (p->taps != 35 || dm != DM_NONE) return -4;
-    constexpr int T = 35, U = pf9_period(35);
+    constexpr int T = 35;
+    const int U = pf9_period(35) + (form == 4 ? 8 : form == 5 ? 16 : 0);
     const int pairs = (p->height + 1) / 2;
-    const int slots = form == 0 ? 256 * 11 : form == 3 ? 256 * 11 : 256 * (form == 1 ? 12 : 14);
+    const int slots = form == 0 || form >= 3 ? 256 * 11 : 256 * (form == 1 ? 12 : 14);
     if (nseg <= 0) nseg = (slots + pairs / 2) / (pairs > 0 ? pairs : 1);
     int seg = ((p->width + nseg - 1) / nseg + U - 1) / U * U;
     if (seg < 2 * U) seg = 2 * U;
@@ -176,6 +177,10 @@ extern "C" int exp_h32(int form, int nseg, int dm, const asw_params *p, const fl
     else if (form == 1) launch_h32<T, 1, DM_NONE, 0, 4, false, 3, 0, true>(p, wl, wr, cin, cout, den, st, seg);
     else if (form == 2) launch_h32<T, 1, DM_NONE, 0, 4, false, 4, 0, true>(p, wl, wr, cin, cout, den, st, seg);
     else if (form == 3) launch_h32<T, 1, DM_NONE, 0, 4, true, 4, 0, true>(p, wl, wr, cin, cout, den, st, seg);
+    // round 6: the shipped form with a deeper cost prefetch (PX more steps: the newest
+    // window element requested P = 5 + PX steps ahead; k_hpass32 waits on vmcnt, not LDS)
+    else if (form == 4) launch_h32<T, 1, DM_NONE, 0, 4, true, 3, 0, true, 8>(p, wl, wr, cin, cout, den, st, seg);
+    else if (form == 5) launch_h32<T, 1, DM_NONE, 0, 4, true, 3, 0, true, 16>(p, wl, wr, cin, cout, den, st, seg);
     else return -4;
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
