@@ -96,11 +96,7 @@ __device__ __forceinline__ void taps32_dl(float &num, float &den, const f4 &wl, 
 // HS: wl / wr are half-size tap-major supports (hs_index below): each staged float4 of
 // an entry is assembled from 4 dwords, the slab in LDS is the same as from the full
 // arrays, so the taps and the outputs are unchanged.
-// DL: the left weights as in k_hpass32<DL>: each lane loads float4 q = lane & 15 of its
-// half's left entry straight into VGPRs (NLD rows ahead) and tap i takes wl_i from lane
-// i/4 of its 16-lane DPP row; the slab holds the right entries only (half the LDS reads).
-template <int T, int NW, int DM, int CP, int NPH, int RB = 2, int PS = 4, bool C16 = false, bool HS = false,
-          bool DL = false>
+template <int T, int NW, int DM, int CP, int NPH, int RB = 2, int PS = 4, bool C16 = false, bool HS = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 4 : 2))) void k_vpass32(
     const float *__restrict__ wl, const float *__restrict__ wr, const float *__restrict__ cin, float *__restrict__ cout,
     float *__restrict__ den, int W, int H, int d_begin, int rows_per_strip, int nxb, int nstrip, int xg_per_xcd) {
@@ -117,9 +113,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     constexpr int LA = cmax(cmax(R + P, LEAD + PS), KD);  // rows past y a step touches
     constexpr int NC = 2 * NW;                             // columns per block
     constexpr int NER = NC + 31;                           // right entries per row
-    constexpr int NE = NER + (DL ? 0 : NC);                // + the left entries (not DL)
-    static_assert(!(DL && HS), "DL reads the full left array");
-    static_assert(!DL || (T + 3) / 4 <= 16, "DL: taps in one DPP row");
+    constexpr int NE = NER + NC;                           // + the left entries
     constexpr int NQ = NE * Q;
     constexpr int NSTAGE = (NQ + NW * 64 - 1) / (NW * 64);
     static_assert(NSTAGE <= 2, "slab row larger than two float4 per thread");
@@ -229,7 +223,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     using PH = Phases<T, NPH>;
     float win[U];
     f4 sa[PS], sb[PS];
-    f4 wlp[DL ? 1 : NPH][PH::NG], wrp[NPH][PH::NG];
+    f4 wlp[NPH][PH::NG], wrp[NPH][PH::NG];
     float dring[KD];
     {
         const int r0 = max(0, y_begin - R);
@@ -259,20 +253,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
     __syncthreads();
     auto request = [&](auto kc, int buf) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
-        if constexpr (!DL) read_wr<T, PH::gb(k), PH::gb(k + 1)>(wlp[k], &slab[buf][my_wl]);
+        read_wr<T, PH::gb(k), PH::gb(k + 1)>(wlp[k], &slab[buf][my_wl]);
         read_wr<T, PH::gb(k), PH::gb(k + 1)>(wrp[k], &slab[buf][my_wr]);
     };
-    // DL: this lane's float4 of its half's left entry at a row (global-address pointer)
-    using gf4 = const __attribute__((address_space(1))) f4;
-    using gfl = const __attribute__((address_space(1))) float;
-    gfl *wlsrc = (gfl *)(wl + (long long)xc * TP + 4 * min(lane & 15, Q - 1));
-    auto wl_load = [&](int row) __attribute__((always_inline)) { return *(gf4 *)(wlsrc + (long long)min(row, H - 1) * wrow); };
-    constexpr int NLD = DL ? ring_div(U, P) : 1;  // left rows in flight (>= the window's P)
-    f4 wld[NLD];
-    if constexpr (DL) {
-#pragma unroll
-        for (int j = 0; j < NLD; ++j) wld[j] = wl_load(y_begin + j);
-    }
     (void)r1;
     request(std::integral_constant<int, 0>{}, 0);
 
@@ -310,11 +293,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 1
                     stage(sa[(s + LEAD) % PS], sb[(s + LEAD) % PS], min(y + LEAD + PS, H - 1));
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if constexpr (DL) taps32_dl<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wld[s % NLD], wrp[k], win);
-                else taps32<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wlp[k], wrp[k], win);
+                taps32<U, s, PH::tb(k), PH::tb(k + 1), DM != DM_READ>(num, dn, wlp[k], wrp[k], win);
                 __builtin_amdgcn_sched_barrier(0);
             });
-            if constexpr (DL) wld[s % NLD] = wl_load(y + NLD);  // row y+NLD's left entry
             if constexpr (DM == DM_READ) {
                 dn = dring[s % KD];
                 dring[s % KD] = bload<CP>(rdn, voff, CLAMP ? (min(y + KD, H - 1) - min(ys + KD, H - 1)) * rowbytes : so);
@@ -571,7 +552,7 @@ __global__ __launch_bounds__(NWB * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 // ---------------------------------------------------------------------------
 // launchers (one (T, DM) per translation unit: build/p32_t<T>_d<DM>.hip)
 // ---------------------------------------------------------------------------
-template <int T, int NW, int DM, int CP, int NPH, bool C16 = false, bool HS = false, bool DL = false>
+template <int T, int NW, int DM, int CP, int NPH, bool C16 = false, bool HS = false>
 void launch_v32(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
                 hipStream_t st) {
     constexpr int U = pf9_period(T);
@@ -590,7 +571,7 @@ void launch_v32(const asw_params *p, const float *wl, const float *wr, const flo
     const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
     nstrip = (H + rows - 1) / rows;
     const int per_xcd = (nxb + 7) / 8;
-    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, 2, 4, C16, HS, DL>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl,
+    hipLaunchKernelGGL((k_vpass32<T, NW, DM, CP, NPH, 2, 4, C16, HS>), dim3(8 * per_xcd * nstrip), dim3(NW * 64), 0, st, wl,
                        wr, cin, cout, den, W, H, p->d_begin, rows, nxb, nstrip, per_xcd);
     note_pass_kernel(ASW_DIR_V, DM, C16 ? "k_vpass32_c16" : "k_vpass32", T,
                      NW == 16 ? (NPH == 4 ? "NW=16,NPH=4" : "NW=16") : "NW=8,NPH=3", CP == kCPStream);

@@ -299,9 +299,7 @@ extern "C" int exp_v32hs(int hs, const asw_params *p, const float *wl, const flo
                          void *stream) {
     hipStream_t st = (hipStream_t)stream;
     if (p->taps != 35) return -4;
-    if (hs == 2) launch_v32<35, 16, DM_NONE, 0, 4, false, false, true>(p, wl, wr, cin, cout, nullptr, st);  // DL
-    else if (hs == 3) launch_v32<35, 16, DM_NONE, 0, 2, false, false, true>(p, wl, wr, cin, cout, nullptr, st);  // DL, 2 phases
-    else if (hs) launch_v32<35, 16, DM_NONE, 0, 4, false, true>(p, wl, wr, cin, cout, nullptr, st);
+    if (hs) launch_v32<35, 16, DM_NONE, 0, 4, false, true>(p, wl, wr, cin, cout, nullptr, st);
     else launch_v32<35, 16, DM_NONE, 0, 4, false, false>(p, wl, wr, cin, cout, nullptr, st);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

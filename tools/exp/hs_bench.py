@@ -23,7 +23,6 @@ from stereo_matchin_amd.synthetic import make_pair  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
-    ap.add_argument("--forms", default="prod,full,half,dl,dl2")
     args = ap.parse_args()
     W, H, D, T = 1920, 1080, 256, 35
     R = T // 2
@@ -62,12 +61,10 @@ def main():
             K.asw_vCostAggregation(p, m.wvl, m.wvr, m.c0, out=out)
         elif form == "full":
             assert lib.exp_v32hs(0, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), cs) == 0
-        elif form == "half":
+        else:
             assert lib.exp_v32hs(1, pp, P(hl), P(hr), P(m.c0), P(out), cs) == 0
-        else:  # the left weights by DPP rows (DL), 4 or 2 weight phases
-            assert lib.exp_v32hs(2 if form == "dl" else 3, pp, P(m.wvl), P(m.wvr), P(m.c0), P(out), cs) == 0
 
-    forms = args.forms.split(",")
+    forms = ["prod", "full", "half"]
     for f in forms:
         out.zero_()
         launch(f)
