@@ -572,8 +572,9 @@ def test_c5_band_oracle_parity(gpu, oracle):
         # 12-column blocks in 3 phases; on this 3840-wide band in XCD-round tiles of 4 plane
         # blocks (v12_tiles in asw_aggregate_impl.h)
         assert names[(0, dm)] == f"{v}<T={T},NW=12,NPH=3,TK=4,DM={dm},nt>", names
-        assert names[(1, dm)].startswith(f"k_hpass11<T={T},NKW={C5_H_NKW},DM={dm}") and \
-            names[(1, dm)].endswith(",nt>"), names
+        # (den-read: the deeper cost prefetch, PX = 24, round 6)
+        h = f"k_hpass11<T={T},NKW={C5_H_NKW}" + (",PX=24" if dm == 2 else "") + f",DM={dm}"
+        assert names[(1, dm)].startswith(h) and names[(1, dm)].endswith(",nt>"), names
     ref = oracle.match(Ls, Rs, D, T, 7, want_cost=True)
     dr, dt = ref["d_ref"], ref["d_tar"]
     assert np.array_equal(_np(res.d_ref), dr) and np.array_equal(_np(res.d_tar), dt)

@@ -304,3 +304,69 @@ extern "C" int exp_v32hs(int hs, const asw_params *p, const float *wl, const flo
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
+
+#ifdef EXP_HPX
+// k_hpass11 den-read with a deeper cost prefetch (PX more steps) and other segment
+// lengths (round 6; the 32-plane H pass gained from PX = 8).  form: T = 51 (C5, 2 plane
+// blocks per block) 0 = shipped (PX 0, 224-column segments), 1 = PX 8 / 256, 2 = PX 0 /
+// 256, 3 = PX 8 / 192, 4 = PX 16 / 288; T = 35 (C4, 4 plane blocks) 10 = shipped
+// (PX 0 / 240), 11 = PX 8 / 240.
+extern "C" int exp_hpx(int form, const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                       float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (form < 10 && p->taps == 51) {
+        constexpr int T = 51;
+        if (form == 0) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 0>(p, wl, wr, cin, cout, den, st, 224);
+        else if (form == 1) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 8>(p, wl, wr, cin, cout, den, st, 256);
+        else if (form == 2) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 0>(p, wl, wr, cin, cout, den, st, 256);
+        else if (form == 3) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 8>(p, wl, wr, cin, cout, den, st, 192);
+        else if (form == 4) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 16>(p, wl, wr, cin, cout, den, st, 288);
+        else if (form == 5) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 16, 8>(p, wl, wr, cin, cout, den, st, 288);
+        else if (form == 6) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 24>(p, wl, wr, cin, cout, den, st, 320);
+        else if (form == 7) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 0, 8>(p, wl, wr, cin, cout, den, st, 224);
+        else if (form == 8) launch_h11<T, 2, DM_READ, kCPStream, kCPStream, 16>(p, wl, wr, cin, cout, den, st, 216);
+        else return -4;
+    } else if (form >= 10 && p->taps == 35) {
+        constexpr int T = 35;
+        if (form == 10) launch_h11<T, 4, DM_READ, kCPStream, kCPStream, 0>(p, wl, wr, cin, cout, den, st, 240);
+        else if (form == 11) launch_h11<T, 4, DM_READ, kCPStream, kCPStream, 8>(p, wl, wr, cin, cout, den, st, 240);
+        else return -4;
+    } else {
+        return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+#endif
+
+#ifdef EXP_C5VPX
+// C5 (T = 51) V den-read, the shipped 12-column tiled shape, with a deeper cost prefetch
+// (PX more steps; round 6, after the H passes gained from it).  px: 0, 8, 16, 24.
+template <int PX>
+static void c5v_px(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
+                   hipStream_t st) {
+    constexpr int T = 51, NW = 12, TK = 4, U = pf9_period(T) + PX;
+    const int W = p->width, H = p->height, Dp = asw_disp_pitch(p), nkb = Dp / 64, nxb = (W + NW - 1) / NW;
+    int nstrip = (int)((2048LL + (long long)nxb * nkb - 1) / ((long long)nxb * nkb));
+    const int max_strip = H / (2 * T) > 1 ? H / (2 * T) : 1;
+    if (nstrip > max_strip) nstrip = max_strip;
+    if (nstrip < 1) nstrip = 1;
+    const int rows = ((H + nstrip - 1) / nstrip + U - 1) / U * U;
+    nstrip = (H + rows - 1) / rows;
+    const int per_xcd = (nxb + 7) / 8;
+    constexpr int TCG = 32 / TK;
+    const int nblocks = 8 * 32 * ((nkb + TK - 1) / TK) * ((per_xcd + TCG - 1) / TCG) * nstrip;
+    hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, 2, kCPStream, kCPStream, 2, 4, TK, 3, PX>), dim3(nblocks),
+                       dim3(NW * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp, p->d_begin, rows, nxb, nstrip, per_xcd);
+}
+extern "C" int exp_c5vpx(int px, const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
+                         float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (p->taps != 51) return -4;
+    if (px == 0) c5v_px<0>(p, wl, wr, cin, cout, den, st);
+    else if (px == 8) c5v_px<8>(p, wl, wr, cin, cout, den, st);
+    else if (px == 16) c5v_px<16>(p, wl, wr, cin, cout, den, st);
+    else if (px == 24) c5v_px<24>(p, wl, wr, cin, cout, den, st);
+    else return -4;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+#endif
