@@ -340,11 +340,13 @@ extern "C" int exp_hpx(int form, const asw_params *p, const float *wl, const flo
 
 #ifdef EXP_C5VPX
 // C5 (T = 51) V den-read, the shipped 12-column tiled shape, with a deeper cost prefetch
-// (PX more steps; round 6, after the H passes gained from it).  px: 0, 8, 16, 24.
-template <int PX>
+// (PX more steps; round 6, after the H passes gained from it) and / or one barrier per
+// row (RB = 1: a 2-row staging ring, 16 fewer VGPRs; the shipped form spills 11 at the
+// 168-VGPR cap of 3 waves per SIMD).  form = PX * 10 + RB.
+template <int PX, int RB>
 static void c5v_px(const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout, float *den,
                    hipStream_t st) {
-    constexpr int T = 51, NW = 12, TK = 4, U = pf9_period(T) + PX;
+    constexpr int T = 51, NW = 12, TK = 4, U = pf9_period(T) + PX, PS = RB == 1 ? 2 : 4;
     const int W = p->width, H = p->height, Dp = asw_disp_pitch(p), nkb = Dp / 64, nxb = (W + NW - 1) / NW;
     int nstrip = (int)((2048LL + (long long)nxb * nkb - 1) / ((long long)nxb * nkb));
     const int max_strip = H / (2 * T) > 1 ? H / (2 * T) : 1;
@@ -355,17 +357,16 @@ static void c5v_px(const asw_params *p, const float *wl, const float *wr, const 
     const int per_xcd = (nxb + 7) / 8;
     constexpr int TCG = 32 / TK;
     const int nblocks = 8 * 32 * ((nkb + TK - 1) / TK) * ((per_xcd + TCG - 1) / TCG) * nstrip;
-    hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, 2, kCPStream, kCPStream, 2, 4, TK, 3, PX>), dim3(nblocks),
+    hipLaunchKernelGGL((k_vpass10<T, NW, DM_READ, RB, kCPStream, kCPStream, 2, PS, TK, 3, PX>), dim3(nblocks),
                        dim3(NW * 64), 0, st, wl, wr, cin, cout, den, W, H, Dp, p->d_begin, rows, nxb, nstrip, per_xcd);
 }
-extern "C" int exp_c5vpx(int px, const asw_params *p, const float *wl, const float *wr, const float *cin, float *cout,
-                         float *den, void *stream) {
+extern "C" int exp_c5vpx(int form, const asw_params *p, const float *wl, const float *wr, const float *cin,
+                         float *cout, float *den, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     if (p->taps != 51) return -4;
-    if (px == 0) c5v_px<0>(p, wl, wr, cin, cout, den, st);
-    else if (px == 8) c5v_px<8>(p, wl, wr, cin, cout, den, st);
-    else if (px == 16) c5v_px<16>(p, wl, wr, cin, cout, den, st);
-    else if (px == 24) c5v_px<24>(p, wl, wr, cin, cout, den, st);
+    if (form == 2) c5v_px<0, 2>(p, wl, wr, cin, cout, den, st);
+    else if (form == 1) c5v_px<0, 1>(p, wl, wr, cin, cout, den, st);
+    else if (form == 81) c5v_px<8, 1>(p, wl, wr, cin, cout, den, st);
     else return -4;
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
