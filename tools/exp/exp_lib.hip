@@ -371,3 +371,19 @@ extern "C" int exp_c5vpx(int form, const asw_params *p, const float *wl, const f
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 #endif
+
+#ifdef EXP_HPXW
+// C5 (T = 51) den-write H pass with the deeper cost prefetch of the shipped den-read form
+// (round 6): form 20 = shipped (PX 0, 224), 21 = PX 24 / 320, 22 = PX 16 / 288
+extern "C" int exp_hpxw(int form, const asw_params *p, const float *wl, const float *wr, const float *cin,
+                        float *cout, float *den, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (p->taps != 51) return -4;
+    constexpr int T = 51;
+    if (form == 20) launch_h11<T, 2, DM_WRITE, kCPStream, kCPStream, 0>(p, wl, wr, cin, cout, den, st, 224);
+    else if (form == 21) launch_h11<T, 2, DM_WRITE, kCPStream, kCPStream, 24>(p, wl, wr, cin, cout, den, st, 320);
+    else if (form == 22) launch_h11<T, 2, DM_WRITE, kCPStream, kCPStream, 16>(p, wl, wr, cin, cout, den, st, 288);
+    else return -4;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+#endif

@@ -42,15 +42,27 @@ def main():
     K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=ref, den=den, den_mode=2)
     torch.cuda.synchronize()
     print("prod", K.pass_kernel(1, 2), flush=True)
-    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp_hpx.so"))
+    wform = any(f >= 20 for f in forms)  # den-write forms (libexp_hpxw.so): out and den checked
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "exp", "libexp_hpxw.so" if wform else "libexp_hpx.so"))
+    if wform:
+        ref_w, den_ref = torch.empty_like(cin), torch.empty_like(cin)
+        K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=ref_w, den=den_ref, den_mode=1)
+        ref, den_o = ref_w, torch.empty_like(cin)
+        del ref_w
+        torch.cuda.synchronize()
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     pp = ctypes.byref(p)
     out = torch.empty_like(cin)
     st = torch.cuda.current_stream()
 
     def launch(f):
-        if f < 0:
+        if f < 0 and wform:
+            K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=out, den=den_o, den_mode=1)
+        elif f < 0:
             K.asw_hCostAggregation(p, m.whl, m.whr, cin, out=out, den=den, den_mode=2)
+        elif wform:
+            rc = lib.exp_hpxw(f, pp, P(m.whl), P(m.whr), P(cin), P(out), P(den_o), ctypes.c_void_p(st.cuda_stream))
+            assert rc == 0, (f, rc)
         else:
             rc = lib.exp_hpx(f, pp, P(m.whl), P(m.whr), P(cin), P(out), P(den), ctypes.c_void_p(st.cuda_stream))
             assert rc == 0, (f, rc)
@@ -60,7 +72,8 @@ def main():
         out.zero_()
         launch(f)
         torch.cuda.synchronize()
-        print(json.dumps({"form": "prod" if f < 0 else f, "bit_exact": bool(torch.equal(out, ref))}), flush=True)
+        ok = bool(torch.equal(out, ref)) and (not wform or bool(torch.equal(den_o, den_ref)))
+        print(json.dumps({"form": "prod" if f < 0 else f, "bit_exact": ok}), flush=True)
     times = {f: [] for f in runs}
     for rep in range(args.reps + 1):
         for f in runs:
