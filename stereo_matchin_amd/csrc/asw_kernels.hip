@@ -146,12 +146,12 @@ __global__ __launch_bounds__(256) void k_raw_cost(const uchar4 *__restrict__ L, 
                 u4 h;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) h[j] = (unsigned short)min(c[j], tau_u);
-                reinterpret_cast<u4 *>(static_cast<unsigned short *>(cost_v) + e0)[q] = h;
+                __builtin_nontemporal_store(h, &reinterpret_cast<u4 *>(static_cast<unsigned short *>(cost_v) + e0)[q]);
             } else {
                 f4 v;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v[j] = 4 * q + j < nloc ? fminf((float)c[j], tau) : 0.0f;
-                reinterpret_cast<f4 *>(static_cast<float *>(cost_v) + e0)[q] = v;
+                __builtin_nontemporal_store(v, &reinterpret_cast<f4 *>(static_cast<float *>(cost_v) + e0)[q]);
             }
         }
     }
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void k_support(SupportJobs jobs, const float *
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             const int e = g * 64 + lane;
-            if (e < nval) out[e] = st[e];
+            if (e < nval) __builtin_nontemporal_store(st[e], &out[e]);  // (nt: write-once stream)
         }
     }
 }
